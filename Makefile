@@ -1,0 +1,30 @@
+# Builds libmiclip.so (HIP/CDNA4, gfx950) in-tree so it travels to the GPU box.
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+PKG      := aihab-clip_amd
+SRC_DIR  := $(PKG)/csrc
+OBJ_DIR  := build/obj
+LIB      := $(PKG)/miclip/libmiclip.so
+SRCS     := $(wildcard $(SRC_DIR)/*.hip)
+OBJS     := $(patsubst $(SRC_DIR)/%.hip,$(OBJ_DIR)/%.o,$(SRCS))
+HDRS     := $(wildcard $(SRC_DIR)/*.h) include/miclip.h
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function \
+            -Wno-unused-variable -Iinclude
+
+all: $(LIB)
+
+$(OBJ_DIR)/%.o: $(SRC_DIR)/%.hip $(HDRS)
+	@mkdir -p $(OBJ_DIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(OBJS) -o $@
+
+asm: $(SRCS)
+	@mkdir -p build/asm
+	for f in $(SRCS); do $(HIPCC) $(HIPFLAGS) --cuda-device-only -S $$f -o build/asm/$$(basename $$f .hip).s; done
+
+clean:
+	rm -rf build $(LIB)
+
+.PHONY: all clean asm

@@ -1,0 +1,198 @@
+// Fused multi-head attention (head dim 64) over the packed QKV projection.
+//
+// Replaces, for one ResidualAttentionBlock, torch's
+//   F.multi_head_attention_forward slow path (q.view(tgt_len, bsz*heads, dh) ->
+//   scaled_dot_product_attention(q, k, v, attn_mask) -> permute back)
+// called from clip/model.py:179-181, with the optional additive causal mask of
+// the text tower (clip/model.py:323-329, -inf strictly above the diagonal).
+// The N x N score matrix is never materialised (online softmax, fp32).
+//
+// CDNA4 design:
+//   * one workgroup per (image, head); the head's whole K and V (N <= 608 keys,
+//     64 dims) are staged once into LDS and shared by all waves;
+//   * each wave owns 32-query chunks; S^T = K . Q^T with
+//     v_mfma_f32_32x32x16 (swapped operands, cdna_hip_programming.md T12): the
+//     query sits on the MFMA lane, so the softmax row max/sum over keys is an
+//     in-register reduction plus one lane^32 exchange;
+//   * the S^T accumulator is converted in place to the B operand of
+//     O^T = V^T . P^T ("accumulator as next operand", §3), and V^T's A
+//     fragments come from the row-major V image through ds_read_b64_tr_b16
+//     (T10) in the permuted k order that the accumulator layout dictates;
+//   * K image XOR-swizzled by (row>>1)&7 (conflict-free ds_read_b128 for the
+//     32x32x16 A fragment), V image by (row&3)<<1 (conflict-free tr reads);
+//     both layouts were checked with an LDS bank model of gfx950's lane groups.
+#include "common.h"
+#include "kernels.h"
+
+namespace miclip {
+
+namespace {
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+template <typename T, bool CAUSAL>
+__global__ __launch_bounds__(1024) void attention_kernel(const T* __restrict__ qkv,
+                                                         T* __restrict__ out, int N, int H,
+                                                         int Npad, int nchunks, float qk_scale) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* kimg = smem;               // [Npad][64] T, 128-B rows
+  char* vimg = smem + Npad * 128;  // [Npad][64] T, 128-B rows
+
+  const int bh = blockIdx.x;
+  const int b = bh / H, h = bh - b * H;
+  const int D = H * 64, ld = 3 * D;
+  const T* base = qkv + (size_t)b * N * ld + h * 64;
+
+  for (int idx = threadIdx.x; idx < Npad * 8; idx += blockDim.x) {
+    const int row = idx >> 3, c = idx & 7;
+    i16x8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (row < N) {
+      kv = *(const i16x8*)(base + (size_t)row * ld + D + c * 8);
+      vv = *(const i16x8*)(base + (size_t)row * ld + 2 * D + c * 8);
+    }
+    *(i16x8*)(kimg + row * 128 + ((c ^ ((row >> 1) & 7)) << 4)) = kv;
+    *(i16x8*)(vimg + row * 128 + ((c ^ ((row & 3) << 1)) << 4)) = vv;
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  // tr-read lane geometry: group g = lane>>4, lane 4q+p of the group
+  const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+  const float c2 = qk_scale * kLog2e;
+
+  for (int chunk = wave; chunk < nchunks; chunk += nw) {
+    const int q = chunk * 32 + l32;
+    i16x8 qf[4];
+    if (q < N) {
+      const T* qp = base + (size_t)q * ld + 8 * hh;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) qf[s] = *(const i16x8*)(qp + 16 * s);
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) qf[s] = i16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+
+    float m = -1e30f, lsum = 0.f;
+    f32x16 o0, o1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; }
+
+    const int nkt_all = Npad >> 5;
+    const int nkt = CAUSAL ? (chunk + 1 < nkt_all ? chunk + 1 : nkt_all) : nkt_all;
+    for (int kt = 0; kt < nkt; ++kt) {
+      // ---- S^T[key][q] = K . Q^T ----
+      f32x16 sacc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+      const int key = kt * 32 + l32;
+      const char* krow = kimg + key * 128;
+      const int ksw = (key >> 1) & 7;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const i16x8 kf = *(const i16x8*)(krow + (((2 * s + hh) ^ ksw) << 4));
+        sacc = Mfma<T>::m32(kf, qf[s], sacc);
+      }
+      // ---- mask, online softmax (fp32, base-2) ----
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kk = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const bool valid = kk < N && (!CAUSAL || kk <= q);
+        sacc[r] = valid ? sacc[r] * c2 : -INFINITY;
+        tmax = fmaxf(tmax, sacc[r]);
+      }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mnew = fmaxf(m, tmax);
+      const float alpha = exp2f(m - mnew);
+      m = mnew;
+      float psum = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sacc[r] = exp2f(sacc[r] - mnew);
+        psum += sacc[r];
+      }
+      lsum = lsum * alpha + psum;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+      // ---- P^T as B operand: k-step s2 uses accumulator regs 8*s2 .. 8*s2+7 ----
+      i16x8 pf[2];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[s2][j] = to_bits<T>(sacc[8 * s2 + j]);
+      // ---- O^T[d][q] += V^T . P^T ----
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          i16x4 lo, hi;
+          {
+            const int kr = kt * 32 + 16 * s2 + 4 * (g >> 1) + tq;
+            const int ch = 4 * dt + 2 * (g & 1) + (tp >> 1);
+            const char* a0 = vimg + kr * 128 + ((ch ^ (tq << 1)) << 4) + 8 * (tp & 1);
+            lo = ds_read_tr16_b64(a0);
+            hi = ds_read_tr16_b64(a0 + 8 * 128);  // rows +8 keep (row & 3)
+          }
+          const i16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          if (dt == 0)
+            o0 = Mfma<T>::m32(vf, pf[s2], o0);
+          else
+            o1 = Mfma<T>::m32(vf, pf[s2], o1);
+        }
+      }
+    }
+
+    lsum += __shfl_xor(lsum, 32, 64);
+    const float inv = 1.0f / lsum;
+    if (q < N) {
+      T* op = out + ((size_t)b * N + q) * D + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) {
+          i16x4 w;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            w[e] = to_bits<T>((dt == 0 ? o0[4 * rg + e] : o1[4 * rg + e]) * inv);
+          *(i16x4*)(op + 32 * dt + 8 * rg + 4 * hh) = w;
+        }
+      }
+    }
+  }
+}
+
+template <typename T, bool CAUSAL>
+hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, hipStream_t s) {
+  const int Npad = (N + 31) & ~31;
+  const int nchunks = Npad / 32;
+  const int per = (nchunks + 15) / 16;
+  const int nw = (nchunks + per - 1) / per;
+  const size_t lds = (size_t)Npad * 256;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  auto kern = attention_kernel<T, CAUSAL>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute(
+        (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(B * H), dim3(nw * 64), lds, s, (const T*)qkv, (T*)out, N, H,
+                     Npad, nchunks, 0.125f);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t attention(int dtype, const void* qkv, void* out, int B, int N, int H, int causal,
+                     hipStream_t s) {
+  if (B < 1 || N < 1 || H < 1) return hipErrorInvalidValue;
+  if (dtype == kF16)
+    return causal ? attn_launch<_Float16, true>(qkv, out, B, N, H, s)
+                  : attn_launch<_Float16, false>(qkv, out, B, N, H, s);
+  return causal ? attn_launch<__bf16, true>(qkv, out, B, N, H, s)
+                : attn_launch<__bf16, false>(qkv, out, B, N, H, s);
+}
+
+}  // namespace miclip

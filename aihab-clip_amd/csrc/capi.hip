@@ -1,0 +1,594 @@
+// C ABI of libmiclip.so (declared in include/miclip.h): model handle, weight
+// repacking, workspaces, and the encode_image / encode_text / zero-shot
+// orchestration over the CDNA4 kernels.
+//
+// Forward schedule of one ResidualAttentionBlock (clip/model.py:183-186), with
+// the residual stream x kept in fp32 [B*N, W] (token-major, i.e. NLD: the
+// reference's LND permutes (clip/model.py:224-226) are a layout choice that
+// does not change per-token arithmetic):
+//   h   = LN1(x)                           layernorm      -> compute dtype
+//   qkv = h . Wqkv^T + b                   gemm_store     [M, 3W]
+//   o   = MHA core(qkv)                    attention      [M, W]
+//   x  += o . Wo^T + bo                    gemm_residual
+//   h   = LN2(x)                           layernorm
+//   f   = QuickGELU(h . Wfc^T + bfc)       gemm_store     [M, 4W]
+//   x  += f . Wp^T + bp                    gemm_residual
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/miclip.h"
+#include "common.h"
+#include "kernels.h"
+
+using namespace miclip;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define MICLIP_HIP(expr)                                                                 \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess)                                                                \
+      return fail(_e == hipErrorInvalidValue ? MICLIP_EINVAL : MICLIP_EHIP,              \
+                  std::string(#expr) + ": " + hipGetErrorString(_e));                    \
+  } while (0)
+
+uint16_t f32_to_bf16_bits(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+uint16_t f32_to_f16_bits(float f) {
+  _Float16 h = (_Float16)f;
+  uint16_t b;
+  std::memcpy(&b, &h, 2);
+  return b;
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+struct Block {
+  void* w_qkv = nullptr;
+  float* b_qkv = nullptr;
+  void* w_out = nullptr;
+  float* b_out = nullptr;
+  void* w_fc = nullptr;
+  float* b_fc = nullptr;
+  void* w_proj = nullptr;
+  float* b_proj = nullptr;
+  float *ln1_g = nullptr, *ln1_b = nullptr, *ln2_g = nullptr, *ln2_b = nullptr;
+};
+
+struct Workspace {
+  int cap_rows = 0;   // token rows
+  int cap_items = 0;  // images or prompts
+  void* patches = nullptr;
+  float* x = nullptr;
+  void* h = nullptr;
+  void* qkv = nullptr;
+  void* o = nullptr;
+  void* f = nullptr;
+  float* feat = nullptr;  // [items, W] fp32 scratch
+  int32_t* rows = nullptr;
+};
+
+}  // namespace
+
+struct miclip_model {
+  miclip_config cfg{};
+  int device = 0;
+  int dtype = 0;
+  int Kp = 0;  // padded patch-GEMM K
+  std::unordered_map<void*, size_t> allocs;
+  int64_t bytes = 0;
+  // tensor name -> (device pointer, numel, kind)
+  struct Slot {
+    void** dst;
+    int64_t numel;
+    int kind;  // 0 = fp32 as-is, 1 = GEMM weight in compute dtype, 2 = conv1 -> [W, Kp]
+    bool loaded;
+    bool visual;
+  };
+  std::unordered_map<std::string, Slot> slots;
+  std::vector<Block> vblocks, tblocks;
+  void* conv_w = nullptr;
+  float *cls = nullptr, *vpos = nullptr, *ln_pre_g = nullptr, *ln_pre_b = nullptr;
+  float *ln_post_g = nullptr, *ln_post_b = nullptr, *vproj = nullptr;
+  float *tok_emb = nullptr, *tpos = nullptr, *ln_final_g = nullptr, *ln_final_b = nullptr;
+  float* text_proj = nullptr;
+  float* logit_scale = nullptr;
+  Workspace wimg, wtxt;
+  // per-kernel-class HIP-event timing (miclip_set_profiling)
+  struct ProfRec {
+    int cls;
+    hipEvent_t a, b;
+    double flops, bytes;
+  };
+  bool profiling = false;
+  std::vector<ProfRec> pending;
+  std::vector<hipEvent_t> event_pool;
+  struct ProfAcc {
+    int64_t launches = 0;
+    double ms = 0, flops = 0, bytes = 0;
+  };
+  std::vector<ProfAcc> prof_acc;
+};
+
+namespace {
+
+enum KClass {
+  K_IM2COL, K_GEMM_PATCH, K_LAYERNORM, K_GEMM_QKV, K_ATTENTION, K_GEMM_OUT, K_GEMM_FC,
+  K_GEMM_PROJ, K_HEAD, K_TEXT_EMBED, K_NUM
+};
+const char* const kClassNames[K_NUM] = {"im2col", "gemm_patch", "layernorm", "gemm_qkv",
+                                        "attention", "gemm_out", "gemm_fc", "gemm_proj",
+                                        "head", "text_embed"};
+
+hipEvent_t take_event(miclip_model* m) {
+  if (!m->event_pool.empty()) {
+    hipEvent_t e = m->event_pool.back();
+    m->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Brackets one launch with events when profiling is on (outside timed runs).
+struct ProfScope {
+  miclip_model* m;
+  int cls;
+  hipStream_t s;
+  double flops, bytes;
+  hipEvent_t a = nullptr;
+  ProfScope(miclip_model* m_, int c, hipStream_t s_, double f, double b)
+      : m(m_), cls(c), s(s_), flops(f), bytes(b) {
+    if (m->profiling && (a = take_event(m))) (void)hipEventRecord(a, s);
+  }
+  ~ProfScope() {
+    if (!a) return;
+    hipEvent_t b = take_event(m);
+    if (!b) return;
+    (void)hipEventRecord(b, s);
+    m->pending.push_back({cls, a, b, flops, bytes});
+  }
+};
+
+int elt() { return 2; }
+
+void add_slot(miclip_model* m, const std::string& name, void** dst, int64_t numel, int kind,
+              bool visual) {
+  m->slots[name] = miclip_model::Slot{dst, numel, kind, false, visual};
+}
+
+void add_block_slots(miclip_model* m, const std::string& prefix, Block& b, int W, bool visual) {
+  add_slot(m, prefix + "attn.in_proj_weight", &b.w_qkv, (int64_t)3 * W * W, 1, visual);
+  add_slot(m, prefix + "attn.in_proj_bias", (void**)&b.b_qkv, 3 * W, 0, visual);
+  add_slot(m, prefix + "attn.out_proj.weight", &b.w_out, (int64_t)W * W, 1, visual);
+  add_slot(m, prefix + "attn.out_proj.bias", (void**)&b.b_out, W, 0, visual);
+  add_slot(m, prefix + "ln_1.weight", (void**)&b.ln1_g, W, 0, visual);
+  add_slot(m, prefix + "ln_1.bias", (void**)&b.ln1_b, W, 0, visual);
+  add_slot(m, prefix + "mlp.c_fc.weight", &b.w_fc, (int64_t)4 * W * W, 1, visual);
+  add_slot(m, prefix + "mlp.c_fc.bias", (void**)&b.b_fc, 4 * W, 0, visual);
+  add_slot(m, prefix + "mlp.c_proj.weight", &b.w_proj, (int64_t)4 * W * W, 1, visual);
+  add_slot(m, prefix + "mlp.c_proj.bias", (void**)&b.b_proj, W, 0, visual);
+  add_slot(m, prefix + "ln_2.weight", (void**)&b.ln2_g, W, 0, visual);
+  add_slot(m, prefix + "ln_2.bias", (void**)&b.ln2_b, W, 0, visual);
+}
+
+int dev_alloc(miclip_model* m, void** p, size_t bytes) {
+  MICLIP_HIP(hipMalloc(p, bytes));
+  m->allocs[*p] = bytes;
+  m->bytes += (int64_t)bytes;
+  return 0;
+}
+
+void dev_free(miclip_model* m, void* p) {
+  if (!p) return;
+  auto it = m->allocs.find(p);
+  if (it != m->allocs.end()) {
+    m->bytes -= (int64_t)it->second;
+    m->allocs.erase(it);
+  }
+  (void)hipFree(p);
+}
+
+bool tower_loaded(const miclip_model* m, bool visual) {
+  for (const auto& kv : m->slots)
+    if (kv.second.visual == visual && !kv.second.loaded && kv.first != "logit_scale")
+      return false;
+  return true;
+}
+
+std::string missing(const miclip_model* m, bool visual) {
+  for (const auto& kv : m->slots)
+    if (kv.second.visual == visual && !kv.second.loaded && kv.first != "logit_scale")
+      return kv.first;
+  return "";
+}
+
+int ensure_ws(miclip_model* m, Workspace& w, int items, int ntok, int W, bool image) {
+  if (items <= w.cap_items) return 0;
+  const int rows = items * ntok;
+  const size_t e = elt();
+  // grow: make sure no queued kernel still uses the old buffers
+  MICLIP_HIP(hipDeviceSynchronize());
+  for (void* p : {w.patches, (void*)w.x, w.h, w.qkv, w.o, w.f, (void*)w.feat, (void*)w.rows})
+    dev_free(m, p);
+  w = Workspace{};
+  int rc;
+  if (image) {
+    const int g = m->cfg.image_resolution / m->cfg.vision_patch_size;
+    if ((rc = dev_alloc(m, &w.patches, (size_t)items * g * g * m->Kp * e))) return rc;
+  }
+  if ((rc = dev_alloc(m, (void**)&w.x, (size_t)rows * W * 4))) return rc;
+  if ((rc = dev_alloc(m, &w.h, (size_t)rows * W * e))) return rc;
+  if ((rc = dev_alloc(m, &w.qkv, (size_t)rows * 3 * W * e))) return rc;
+  if ((rc = dev_alloc(m, &w.o, (size_t)rows * W * e))) return rc;
+  if ((rc = dev_alloc(m, &w.f, (size_t)rows * 4 * W * e))) return rc;
+  if ((rc = dev_alloc(m, (void**)&w.feat, (size_t)items * W * 4))) return rc;
+  if ((rc = dev_alloc(m, (void**)&w.rows, (size_t)items * 4))) return rc;
+  w.cap_items = items;
+  w.cap_rows = rows;
+  return 0;
+}
+
+// Algorithmic cost of one GEMM launch: 2MNK flops; bytes = read A and W once,
+// write C (2 B/elt), plus the fp32 residual read+write for residual epilogues.
+double gemm_flops(double M, double N, double K) { return 2.0 * M * N * K; }
+double gemm_bytes(double M, double N, double K, double c_bytes) {
+  return 2.0 * M * K + 2.0 * N * K + c_bytes * M * N;
+}
+
+int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, int W, int H,
+              int causal, hipStream_t s) {
+  const int M = items * N, dt = m->dtype;
+  const double dM = M, dW = W;
+  {
+    ProfScope p(m, K_LAYERNORM, s, 0, dM * dW * 6);
+    MICLIP_HIP(layernorm(dt, w.x, nullptr, 1, b.ln1_g, b.ln1_b, nullptr, w.h, M, W, 0, s));
+  }
+  {
+    ProfScope p(m, K_GEMM_QKV, s, gemm_flops(dM, 3 * dW, dW), gemm_bytes(dM, 3 * dW, dW, 2));
+    MICLIP_HIP(gemm_store(dt, w.h, b.w_qkv, b.b_qkv, w.qkv, M, 3 * W, W, ACT_NONE, s));
+  }
+  {
+    const double n = N;
+    ProfScope p(m, K_ATTENTION, s, 4.0 * items * H * n * n * 64, dM * dW * 2 * 4);
+    MICLIP_HIP(attention(dt, w.qkv, w.o, items, N, H, causal, s));
+  }
+  {
+    ProfScope p(m, K_GEMM_OUT, s, gemm_flops(dM, dW, dW), gemm_bytes(dM, dW, dW, 8));
+    MICLIP_HIP(gemm_residual(dt, w.o, b.w_out, b.b_out, w.x, M, W, W, s));
+  }
+  {
+    ProfScope p(m, K_LAYERNORM, s, 0, dM * dW * 6);
+    MICLIP_HIP(layernorm(dt, w.x, nullptr, 1, b.ln2_g, b.ln2_b, nullptr, w.h, M, W, 0, s));
+  }
+  {
+    ProfScope p(m, K_GEMM_FC, s, gemm_flops(dM, 4 * dW, dW), gemm_bytes(dM, 4 * dW, dW, 2));
+    MICLIP_HIP(gemm_store(dt, w.h, b.w_fc, b.b_fc, w.f, M, 4 * W, W, m->cfg.act, s));
+  }
+  {
+    ProfScope p(m, K_GEMM_PROJ, s, gemm_flops(dM, dW, 4 * dW), gemm_bytes(dM, dW, 4 * dW, 8));
+    MICLIP_HIP(gemm_residual(dt, w.f, b.w_proj, b.b_proj, w.x, M, W, 4 * W, s));
+  }
+  return 0;
+}
+
+bool cfg_ok(const miclip_config& c, std::string& why) {
+  auto bad = [&](const char* w) { why = w; return false; };
+  if (c.vision_width % 256 || c.vision_width < 256 || c.vision_width > 1536)
+    return bad("vision_width must be a multiple of 256 in [256, 1536]");
+  if (c.transformer_width % 256 || c.transformer_width < 256 || c.transformer_width > 1536)
+    return bad("transformer_width must be a multiple of 256 in [256, 1536]");
+  if (c.transformer_heads * 64 != c.transformer_width)
+    return bad("transformer_heads * 64 must equal transformer_width (head dim 64)");
+  if (c.vision_patch_size < 1 || c.image_resolution % c.vision_patch_size)
+    return bad("image_resolution must be a multiple of vision_patch_size");
+  const int g = c.image_resolution / c.vision_patch_size;
+  if ((g * g + 1 + 31) / 32 * 32 * 256 > 160 * 1024)
+    return bad("too many vision tokens for the attention kernel (max 640)");
+  if (c.context_length < 1 || c.context_length > 640) return bad("context_length out of range");
+  if (c.vision_layers < 1 || c.transformer_layers < 0) return bad("bad layer count");
+  if (c.embed_dim < 1 || c.vocab_size < 1) return bad("bad embed_dim / vocab_size");
+  if (c.compute_dtype != MICLIP_FP16 && c.compute_dtype != MICLIP_BF16)
+    return bad("compute_dtype must be MICLIP_FP16 or MICLIP_BF16");
+  if (c.act != MICLIP_ACT_QUICKGELU && c.act != MICLIP_ACT_GELU) return bad("bad act");
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* miclip_last_error(void) { return g_last_error.c_str(); }
+int miclip_abi_version(void) { return MICLIP_ABI_VERSION; }
+
+int miclip_model_create(const miclip_config* cfg, int device, miclip_model** out) {
+  if (!cfg || !out) return fail(MICLIP_EINVAL, "null argument");
+  std::string why;
+  if (!cfg_ok(*cfg, why)) return fail(MICLIP_EINVAL, "invalid config: " + why);
+  int ndev = 0;
+  MICLIP_HIP(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(MICLIP_EINVAL, "invalid device index");
+  MICLIP_HIP(hipSetDevice(device));
+  auto* m = new miclip_model();
+  m->cfg = *cfg;
+  m->device = device;
+  m->dtype = cfg->compute_dtype;
+  const int P = cfg->vision_patch_size, Wv = cfg->vision_width, Wt = cfg->transformer_width;
+  m->Kp = (3 * P * P + 63) / 64 * 64;
+  const int g = cfg->image_resolution / P, N = g * g + 1, E = cfg->embed_dim;
+  m->vblocks.resize(cfg->vision_layers);
+  m->tblocks.resize(cfg->transformer_layers);
+  add_slot(m, "positional_embedding", (void**)&m->tpos, (int64_t)cfg->context_length * Wt, 0, false);
+  add_slot(m, "text_projection", (void**)&m->text_proj, (int64_t)Wt * E, 0, false);
+  add_slot(m, "logit_scale", (void**)&m->logit_scale, 1, 0, false);
+  add_slot(m, "visual.class_embedding", (void**)&m->cls, Wv, 0, true);
+  add_slot(m, "visual.positional_embedding", (void**)&m->vpos, (int64_t)N * Wv, 0, true);
+  add_slot(m, "visual.proj", (void**)&m->vproj, (int64_t)Wv * E, 0, true);
+  add_slot(m, "visual.conv1.weight", &m->conv_w, (int64_t)Wv * 3 * P * P, 2, true);
+  add_slot(m, "visual.ln_pre.weight", (void**)&m->ln_pre_g, Wv, 0, true);
+  add_slot(m, "visual.ln_pre.bias", (void**)&m->ln_pre_b, Wv, 0, true);
+  add_slot(m, "visual.ln_post.weight", (void**)&m->ln_post_g, Wv, 0, true);
+  add_slot(m, "visual.ln_post.bias", (void**)&m->ln_post_b, Wv, 0, true);
+  for (int i = 0; i < cfg->vision_layers; ++i)
+    add_block_slots(m, "visual.transformer.resblocks." + std::to_string(i) + ".", m->vblocks[i],
+                    Wv, true);
+  for (int i = 0; i < cfg->transformer_layers; ++i)
+    add_block_slots(m, "transformer.resblocks." + std::to_string(i) + ".", m->tblocks[i], Wt,
+                    false);
+  add_slot(m, "token_embedding.weight", (void**)&m->tok_emb, (int64_t)cfg->vocab_size * Wt, 0,
+           false);
+  add_slot(m, "ln_final.weight", (void**)&m->ln_final_g, Wt, 0, false);
+  add_slot(m, "ln_final.bias", (void**)&m->ln_final_b, Wt, 0, false);
+  *out = m;
+  return 0;
+}
+
+int miclip_model_load_weights(miclip_model* m, const miclip_tensor* t, int32_t n) {
+  if (!m || (!t && n)) return fail(MICLIP_EINVAL, "null argument");
+  MICLIP_HIP(hipSetDevice(m->device));
+  std::vector<uint16_t> tmp;
+  for (int i = 0; i < n; ++i) {
+    if (!t[i].name || !t[i].data) return fail(MICLIP_EINVAL, "null tensor name/data");
+    auto it = m->slots.find(t[i].name);
+    if (it == m->slots.end())
+      return fail(MICLIP_EINVAL, std::string("unexpected key in state_dict: ") + t[i].name);
+    auto& slot = it->second;
+    if (t[i].numel != slot.numel)
+      return fail(MICLIP_EINVAL, std::string("size mismatch for ") + t[i].name + ": got " +
+                                     std::to_string(t[i].numel) + ", expected " +
+                                     std::to_string(slot.numel));
+    int rc;
+    if (slot.kind == 0) {
+      if (!*slot.dst && (rc = dev_alloc(m, slot.dst, (size_t)slot.numel * 4))) return rc;
+      MICLIP_HIP(hipMemcpy(*slot.dst, t[i].data, (size_t)slot.numel * 4, hipMemcpyHostToDevice));
+    } else {
+      int64_t rows = 0, cols = 0, src_cols = 0;
+      if (slot.kind == 1) {
+        // nn.Linear / in_proj weight [out, in]: already the W[N][K] operand layout
+        const std::string nm = it->first;
+        const bool is_cproj = nm.find("c_proj") != std::string::npos;
+        const int W = slot.visual ? m->cfg.vision_width : m->cfg.transformer_width;
+        cols = is_cproj ? 4 * W : W;
+        rows = slot.numel / cols;
+        src_cols = cols;
+      } else {
+        // conv1.weight [W, 3, P, P] -> [W, Kp] zero-padded (col = c*P*P + ky*P + kx)
+        const int P = m->cfg.vision_patch_size;
+        rows = m->cfg.vision_width;
+        src_cols = 3 * P * P;
+        cols = m->Kp;
+      }
+      tmp.assign((size_t)rows * cols, 0);
+      for (int64_t r = 0; r < rows; ++r)
+        for (int64_t c = 0; c < src_cols; ++c) {
+          const float v = t[i].data[r * src_cols + c];
+          tmp[r * cols + c] = m->dtype == MICLIP_FP16 ? f32_to_f16_bits(v) : f32_to_bf16_bits(v);
+        }
+      if (!*slot.dst && (rc = dev_alloc(m, slot.dst, tmp.size() * 2))) return rc;
+      MICLIP_HIP(hipMemcpy(*slot.dst, tmp.data(), tmp.size() * 2, hipMemcpyHostToDevice));
+    }
+    slot.loaded = true;
+  }
+  return 0;
+}
+
+int miclip_reserve(miclip_model* m, int32_t max_images, int32_t max_prompts) {
+  if (!m || max_images < 0 || max_prompts < 0) return fail(MICLIP_EINVAL, "bad argument");
+  MICLIP_HIP(hipSetDevice(m->device));
+  const int g = m->cfg.image_resolution / m->cfg.vision_patch_size;
+  int rc;
+  if (max_images &&
+      (rc = ensure_ws(m, m->wimg, max_images, g * g + 1, m->cfg.vision_width, true)))
+    return rc;
+  if (max_prompts && (rc = ensure_ws(m, m->wtxt, max_prompts, m->cfg.context_length,
+                                     m->cfg.transformer_width, false)))
+    return rc;
+  return 0;
+}
+
+int miclip_encode_image(miclip_model* m, const float* images, int32_t B, float* out,
+                        uint32_t flags, void* stream) {
+  if (!m || !images || !out || B < 1) return fail(MICLIP_EINVAL, "bad argument to encode_image");
+  if (!tower_loaded(m, true))
+    return fail(MICLIP_ENOWEIGHTS, "visual weights not loaded (missing " + missing(m, true) + ")");
+  hipStream_t s = (hipStream_t)stream;
+  const auto& c = m->cfg;
+  const int P = c.vision_patch_size, R = c.image_resolution, W = c.vision_width;
+  const int g = R / P, np = g * g, N = np + 1, H = W / 64, dt = m->dtype;
+  int rc;
+  if ((rc = ensure_ws(m, m->wimg, B, N, W, true))) return rc;
+  Workspace& w = m->wimg;
+  const int M = B * N;
+  {
+    ProfScope p(m, K_IM2COL, s, 0, (double)B * 3 * R * R * 4 + (double)B * np * m->Kp * 2);
+    MICLIP_HIP(im2col(dt, images, w.patches, B, R, P, m->Kp, s));
+  }
+  {
+    const double dM = (double)B * np;
+    ProfScope p(m, K_GEMM_PATCH, s, gemm_flops(dM, W, 3.0 * P * P), gemm_bytes(dM, W, m->Kp, 4));
+    MICLIP_HIP(gemm_patch(dt, w.patches, m->conv_w, m->vpos, w.x, B * np, W, m->Kp, np, s));
+  }
+  {
+    ProfScope p(m, K_LAYERNORM, s, 0, (double)M * W * 8);
+    MICLIP_HIP(class_token(m->cls, m->vpos, w.x, B, N, W, s));
+    MICLIP_HIP(layernorm(dt, w.x, nullptr, 1, m->ln_pre_g, m->ln_pre_b, w.x, nullptr, M, W, 0, s));
+  }
+  for (int l = 0; l < c.vision_layers; ++l)
+    if ((rc = run_block(m, m->vblocks[l], w, B, N, W, H, 0, s))) return rc;
+  const bool proj = flags & MICLIP_FLAG_APPLY_PROJ, norm = flags & MICLIP_FLAG_NORMALIZE;
+  // ln_post on the CLS rows only (clip/model.py:228): rows b*N
+  ProfScope p(m, K_HEAD, s, proj ? 2.0 * B * W * c.embed_dim : 0.0, (double)B * W * 8);
+  if (!proj) {
+    MICLIP_HIP(layernorm(dt, w.x, nullptr, N, m->ln_post_g, m->ln_post_b, out, nullptr, B, W,
+                         norm ? 1 : 0, s));
+  } else {
+    MICLIP_HIP(layernorm(dt, w.x, nullptr, N, m->ln_post_g, m->ln_post_b, w.feat, nullptr, B, W,
+                         0, s));
+    MICLIP_HIP(rowvec_matmul(w.feat, m->vproj, out, B, W, c.embed_dim, s));
+    if (norm) MICLIP_HIP(row_l2norm(out, B, c.embed_dim, s));
+  }
+  return 0;
+}
+
+int miclip_encode_text(miclip_model* m, const int64_t* tokens, int32_t P, float* x_before,
+                       float* x_proj, void* stream) {
+  if (!m || !tokens || P < 1) return fail(MICLIP_EINVAL, "bad argument to encode_text");
+  if (!tower_loaded(m, false))
+    return fail(MICLIP_ENOWEIGHTS, "text weights not loaded (missing " + missing(m, false) + ")");
+  hipStream_t s = (hipStream_t)stream;
+  const auto& c = m->cfg;
+  const int L = c.context_length, W = c.transformer_width, H = c.transformer_heads;
+  int rc;
+  if ((rc = ensure_ws(m, m->wtxt, P, L, W, false))) return rc;
+  Workspace& w = m->wtxt;
+  {
+    ProfScope p(m, K_TEXT_EMBED, s, 0, (double)P * L * W * 12);
+    MICLIP_HIP(token_embed(tokens, m->tok_emb, m->tpos, w.x, w.rows, P, L, W, c.vocab_size, s));
+  }
+  for (int l = 0; l < c.transformer_layers; ++l)
+    if ((rc = run_block(m, m->tblocks[l], w, P, L, W, H, 1, s))) return rc;
+  float* xb = x_before ? x_before : w.feat;
+  ProfScope p(m, K_HEAD, s, x_proj ? 2.0 * P * W * c.embed_dim : 0.0, (double)P * W * 8);
+  MICLIP_HIP(layernorm(m->dtype, w.x, w.rows, 0, m->ln_final_g, m->ln_final_b, xb, nullptr, P, W,
+                       0, s));
+  if (x_proj) MICLIP_HIP(rowvec_matmul(xb, m->text_proj, x_proj, P, W, c.embed_dim, s));
+  return 0;
+}
+
+int miclip_zero_shot(miclip_model* m, const float* feats, int32_t B, int32_t apply_proj,
+                     const float* text_weights, int32_t C, float scale, float* logits,
+                     int32_t* topk, int32_t k, void* stream) {
+  if (!m || !feats || !text_weights || !logits || B < 1 || C < 1 || k < 0 || k > C)
+    return fail(MICLIP_EINVAL, "bad argument to zero_shot");
+  if (apply_proj && !m->slots["visual.proj"].loaded)
+    return fail(MICLIP_ENOWEIGHTS, "visual.proj not loaded");
+  const int E = m->cfg.embed_dim;
+  const int Din = apply_proj ? m->cfg.vision_width : E;
+  MICLIP_HIP(zero_shot(feats, apply_proj ? m->vproj : nullptr, text_weights, logits,
+                       topk, B, Din, E, C, scale, topk ? k : 0, (hipStream_t)stream));
+  return 0;
+}
+
+int miclip_set_profiling(miclip_model* m, int enable) {
+  if (!m) return fail(MICLIP_EINVAL, "null model");
+  m->profiling = enable != 0;
+  return 0;
+}
+
+int miclip_profile_read(miclip_model* m, miclip_kernel_stat* out, int32_t n, int32_t reset) {
+  if (!m) return fail(MICLIP_EINVAL, "null model");
+  if ((int)m->prof_acc.size() < K_NUM) m->prof_acc.resize(K_NUM);
+  for (auto& r : m->pending) {
+    MICLIP_HIP(hipEventSynchronize(r.b));
+    float ms = 0.f;
+    MICLIP_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+    auto& acc = m->prof_acc[r.cls];
+    acc.launches += 1;
+    acc.ms += ms;
+    acc.flops += r.flops;
+    acc.bytes += r.bytes;
+    m->event_pool.push_back(r.a);
+    m->event_pool.push_back(r.b);
+  }
+  m->pending.clear();
+  for (int i = 0; i < K_NUM && i < n && out; ++i) {
+    out[i].name = kClassNames[i];
+    out[i].launches = m->prof_acc[i].launches;
+    out[i].ms = m->prof_acc[i].ms;
+    out[i].flops = m->prof_acc[i].flops;
+    out[i].bytes = m->prof_acc[i].bytes;
+  }
+  if (reset) m->prof_acc.assign(K_NUM, miclip_model::ProfAcc{});
+  return K_NUM;
+}
+
+void miclip_model_destroy(miclip_model* m) {
+  if (!m) return;
+  (void)hipSetDevice(m->device);
+  for (auto& r : m->pending) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  for (hipEvent_t e : m->event_pool) (void)hipEventDestroy(e);
+  for (auto& kv : m->allocs) (void)hipFree(kv.first);
+  delete m;
+}
+
+int64_t miclip_model_bytes(const miclip_model* m) { return m ? m->bytes : 0; }
+
+int miclip_op_gemm(int32_t dtype, const void* A, const void* W, const float* bias, void* C,
+                   int32_t M, int32_t N, int32_t K, int32_t epi, int32_t act, void* stream) {
+  if (!A || !W || !C) return fail(MICLIP_EINVAL, "null argument");
+  hipStream_t s = (hipStream_t)stream;
+  if (epi == 0) {
+    MICLIP_HIP(gemm_store(dtype, A, W, bias, C, M, N, K, act, s));
+  } else if (epi == 1) {
+    if (!bias) return fail(MICLIP_EINVAL, "residual epilogue needs a bias");
+    MICLIP_HIP(gemm_residual(dtype, A, W, bias, (float*)C, M, N, K, s));
+  } else if (epi == 2) {
+    MICLIP_HIP(gemm_f32(dtype, A, W, bias, (float*)C, M, N, K, s));
+  } else {
+    return fail(MICLIP_EINVAL, "unknown epilogue");
+  }
+  return 0;
+}
+
+int miclip_op_layernorm(int32_t dtype, const float* in, const float* gamma, const float* beta,
+                        void* out, int32_t out_is_f32, int32_t R, int32_t D, void* stream) {
+  if (!in || !gamma || !beta || !out) return fail(MICLIP_EINVAL, "null argument");
+  MICLIP_HIP(layernorm(dtype, in, nullptr, 1, gamma, beta, out_is_f32 ? (float*)out : nullptr,
+                       out_is_f32 ? nullptr : out, R, D, 0, (hipStream_t)stream));
+  return 0;
+}
+
+int miclip_op_attention(int32_t dtype, const void* qkv, void* out, int32_t B, int32_t N,
+                        int32_t H, int32_t causal, void* stream) {
+  if (!qkv || !out) return fail(MICLIP_EINVAL, "null argument");
+  MICLIP_HIP(attention(dtype, qkv, out, B, N, H, causal, (hipStream_t)stream));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,94 @@
+// Shared device helpers for the miclip CDNA4 (gfx950) kernels.
+//
+// Compute dtype T is either _Float16 (the reference's GPU precision:
+// convert_weights, clip/model.py:372-393) or __bf16. Both run on the same
+// MFMA rate on gfx950; accumulation, LayerNorm statistics, softmax and the
+// residual stream are fp32 everywhere.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MICLIP_DEV __device__ __forceinline__
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x8 __attribute__((ext_vector_type(8)));
+typedef short i16x4_vs __attribute__((__vector_size__(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#define LDS_AS __attribute__((address_space(3)))
+#define GLB_AS __attribute__((address_space(1)))
+
+namespace miclip {
+
+enum DType { kF16 = 0, kBF16 = 1 };
+
+template <typename T> struct Mfma;
+
+template <> struct Mfma<_Float16> {
+  typedef f16x8 v8;
+  static MICLIP_DEV f32x4 m16(const i16x8& a, const i16x8& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  }
+  static MICLIP_DEV f32x16 m32(const i16x8& a, const i16x8& b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  }
+};
+
+template <> struct Mfma<__bf16> {
+  typedef bf16x8 v8;
+  static MICLIP_DEV f32x4 m16(const i16x8& a, const i16x8& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  }
+  static MICLIP_DEV f32x16 m32(const i16x8& a, const i16x8& b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  }
+};
+
+// float <-> storage type (round to nearest even; the compiler emits v_cvt_pk_*)
+template <typename T> MICLIP_DEV T to_t(float x) { return static_cast<T>(x); }
+template <typename T> MICLIP_DEV float to_f(T x) { return static_cast<float>(x); }
+template <typename T> MICLIP_DEV short to_bits(float x) {
+  return __builtin_bit_cast(short, static_cast<T>(x));
+}
+template <typename T> MICLIP_DEV float from_bits(short b) {
+  return static_cast<float>(__builtin_bit_cast(T, b));
+}
+
+MICLIP_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+MICLIP_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// 16-byte async global -> LDS copy (global_load_lds_dwordx4). LDS destination is
+// the wave-uniform `lds` base + lane*16; the global source is per lane.
+MICLIP_DEV void glds16(const void* g, void* lds) {
+  __builtin_amdgcn_global_load_lds((const GLB_AS void*)g, (LDS_AS void*)lds, 16, 0, 0);
+}
+
+MICLIP_DEV i16x4 ds_read_tr16_b64(const void* lds) {
+  return __builtin_bit_cast(
+      i16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4_vs*)(lds)));
+}
+
+// Bijective XCD-aware block remap (cdna_hip_programming.md §5.5 T1): blocks that
+// the dispatcher deals to one XCD (b, b+8, ...) get a contiguous range of tiles.
+MICLIP_DEV int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+}  // namespace miclip

@@ -1,0 +1,212 @@
+// Embedding, gather and head kernels around the transformer stacks.
+//
+//   im2col       conv1 patchify as a GEMM operand (clip/model.py:204, 217-219)
+//   class_token  class-embedding row + pos[0] (clip/model.py:220-221)
+//   token_embed  token_embedding(text) + positional_embedding and the EOT index
+//                text.argmax(-1) (clip/model.py:339-341, 350)
+//   rowvec_matmul  x_before @ text_projection (clip/model.py:351), fp32
+//   zero_shot    x @ visual.proj -> F.normalize -> scale * f @ text_weights -> topk
+//                (methods/ProLIP.py:38-41, 288-293; methods/utils.py:16-21), fp32
+// All of these are small next to the transformer blocks; they are written for
+// coalesced access and one launch each, not for MFMA.
+#include "common.h"
+#include "kernels.h"
+
+namespace miclip {
+
+namespace {
+
+template <typename T>
+__global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ img,
+                                                     T* __restrict__ patches, int R, int P,
+                                                     int Kp) {
+  const int g = R / P, np = g * g;
+  const int row = blockIdx.x;  // b*np + py*g + px
+  const int b = row / np, pi = row - b * np;
+  const int py = pi / g, px = pi - py * g;
+  const int PP = P * P, K = 3 * PP;
+  const float* src = img + (size_t)b * 3 * R * R + (size_t)(py * P) * R + px * P;
+  T* dst = patches + (size_t)row * Kp;
+  for (int col = threadIdx.x; col < Kp; col += blockDim.x) {
+    float v = 0.f;
+    if (col < K) {
+      const int c = col / PP, rem = col - c * PP;
+      const int ky = rem / P, kx = rem - ky * P;
+      v = src[(size_t)c * R * R + ky * R + kx];
+    }
+    dst[col] = to_t<T>(v);
+  }
+}
+
+__global__ __launch_bounds__(256) void class_token_kernel(const float* __restrict__ cls,
+                                                          const float* __restrict__ pos,
+                                                          float* __restrict__ X, int ntok,
+                                                          int D) {
+  float* dst = X + (size_t)blockIdx.x * ntok * D;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) dst[d] = cls[d] + pos[d];
+}
+
+__global__ __launch_bounds__(256) void token_embed_kernel(const int64_t* __restrict__ tokens,
+                                                          const float* __restrict__ emb,
+                                                          const float* __restrict__ pos,
+                                                          float* __restrict__ X, int L, int D,
+                                                          int vocab) {
+  const int row = blockIdx.x, t = row % L;
+  int64_t id = tokens[row];
+  id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);  // ids are validated on the host
+  const float* e = emb + (size_t)id * D;
+  const float* p = pos + (size_t)t * D;
+  float* dst = X + (size_t)row * D;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) dst[d] = e[d] + p[d];
+}
+
+// one wave per prompt: first index of the maximum token id (torch.argmax)
+__global__ __launch_bounds__(64) void eot_kernel(const int64_t* __restrict__ tokens,
+                                                 int32_t* __restrict__ eot_rows, int L) {
+  const int p = blockIdx.x, lane = threadIdx.x;
+  int64_t best = INT64_MIN;
+  int bi = 0x7fffffff;
+  for (int t = lane; t < L; t += 64) {
+    const int64_t v = tokens[(size_t)p * L + t];
+    if (v > best) { best = v; bi = t; }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const int64_t ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+  }
+  if (lane == 0) eot_rows[p] = p * L + bi;
+}
+
+__global__ __launch_bounds__(256) void rowvec_matmul_kernel(const float* __restrict__ in,
+                                                            const float* __restrict__ Wm,
+                                                            float* __restrict__ out, int D,
+                                                            int E) {
+  extern __shared__ float xs[];
+  const int r = blockIdx.y;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) xs[d] = in[(size_t)r * D + d];
+  __syncthreads();
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E) return;
+  float acc = 0.f;
+  for (int d = 0; d < D; ++d) acc = fmaf(xs[d], Wm[(size_t)d * E + e], acc);
+  out[(size_t)r * E + e] = acc;
+}
+
+__global__ __launch_bounds__(256) void zero_shot_kernel(const float* __restrict__ x,
+                                                        const float* __restrict__ proj,
+                                                        const float* __restrict__ tw,
+                                                        float* __restrict__ logits,
+                                                        int32_t* __restrict__ topk, int Din,
+                                                        int E, int C, float scale, int k) {
+  extern __shared__ float sm[];
+  float* xs = sm;          // Din
+  float* fs = xs + Din;    // E
+  float* ls = fs + E;      // C
+  float* red = ls + C;     // 4
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int d = tid; d < Din; d += 256) xs[d] = x[(size_t)b * Din + d];
+  __syncthreads();
+  float n2 = 0.f;
+  for (int e = tid; e < E; e += 256) {
+    float acc;
+    if (proj) {
+      acc = 0.f;
+      for (int d = 0; d < Din; ++d) acc = fmaf(xs[d], proj[(size_t)d * E + e], acc);
+    } else {
+      acc = xs[e];
+    }
+    fs[e] = acc;
+    n2 += acc * acc;
+  }
+  n2 = wave_sum(n2);
+  if (lane == 0) red[w] = n2;
+  __syncthreads();
+  const float inv = 1.0f / fmaxf(sqrtf(red[0] + red[1] + red[2] + red[3]), 1e-12f);
+  for (int c = tid; c < C; c += 256) {
+    float acc = 0.f;
+    for (int e = 0; e < E; ++e) acc = fmaf(fs[e] * inv, tw[(size_t)e * C + c], acc);
+    ls[c] = scale * acc;
+    logits[(size_t)b * C + c] = scale * acc;
+  }
+  __syncthreads();
+  if (tid == 0 && topk) {
+    // selection of the k largest, ties -> lower index first (sorted, largest first)
+    for (int j = 0; j < k; ++j) {
+      int bi = -1;
+      float bv = -INFINITY;
+      for (int c = 0; c < C; ++c) {
+        const float v = ls[c];
+        if (bi < 0 || v > bv) { bv = v; bi = c; }
+      }
+      topk[(size_t)b * k + j] = bi;
+      ls[bi] = -INFINITY;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void row_l2norm_kernel(float* __restrict__ x, int D) {
+  float* row = x + (size_t)blockIdx.x * D;
+  float n2 = 0.f;
+  for (int d = threadIdx.x; d < D; d += 64) n2 += row[d] * row[d];
+  const float inv = 1.0f / fmaxf(sqrtf(wave_sum(n2)), 1e-12f);
+  for (int d = threadIdx.x; d < D; d += 64) row[d] *= inv;
+}
+
+}  // namespace
+
+hipError_t row_l2norm(float* x, int R, int D, hipStream_t s) {
+  if (R < 1 || D < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(row_l2norm_kernel, dim3(R), dim3(64), 0, s, x, D);
+  return hipGetLastError();
+}
+
+hipError_t im2col(int dtype, const float* img, void* patches, int B, int R, int P, int Kp,
+                  hipStream_t s) {
+  if (B < 1 || P < 1 || R % P || Kp < 3 * P * P) return hipErrorInvalidValue;
+  const int np = (R / P) * (R / P);
+  if (dtype == kF16)
+    hipLaunchKernelGGL(im2col_kernel<_Float16>, dim3(B * np), dim3(256), 0, s, img,
+                       (_Float16*)patches, R, P, Kp);
+  else
+    hipLaunchKernelGGL(im2col_kernel<__bf16>, dim3(B * np), dim3(256), 0, s, img,
+                       (__bf16*)patches, R, P, Kp);
+  return hipGetLastError();
+}
+
+hipError_t class_token(const float* cls, const float* pos, float* X, int B, int ntok, int D,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(class_token_kernel, dim3(B), dim3(256), 0, s, cls, pos, X, ntok, D);
+  return hipGetLastError();
+}
+
+hipError_t token_embed(const int64_t* tokens, const float* tok_emb, const float* pos, float* X,
+                       int32_t* eot_rows, int P, int L, int D, int vocab, hipStream_t s) {
+  if (P < 1 || L < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(token_embed_kernel, dim3(P * L), dim3(256), 0, s, tokens, tok_emb, pos, X,
+                     L, D, vocab);
+  hipLaunchKernelGGL(eot_kernel, dim3(P), dim3(64), 0, s, tokens, eot_rows, L);
+  return hipGetLastError();
+}
+
+hipError_t rowvec_matmul(const float* in, const float* Wm, float* out, int R, int D, int E,
+                         hipStream_t s) {
+  if (R < 1 || D < 1 || E < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rowvec_matmul_kernel, dim3((E + 255) / 256, R), dim3(256),
+                     D * sizeof(float), s, in, Wm, out, D, E);
+  return hipGetLastError();
+}
+
+hipError_t zero_shot(const float* x, const float* proj, const float* tw, float* logits,
+                     int32_t* topk, int B, int Din, int E, int C, float scale, int k,
+                     hipStream_t s) {
+  if (B < 1 || C < 1 || E < 1 || k < 0 || k > C || (!proj && Din != E)) return hipErrorInvalidValue;
+  const size_t sm = (size_t)(Din + E + C + 4) * sizeof(float);
+  if (sm > 64 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(zero_shot_kernel, dim3(B), dim3(256), sm, s, x, proj, tw, logits, topk, Din,
+                     E, C, scale, k);
+  return hipGetLastError();
+}
+
+}  // namespace miclip

@@ -1,0 +1,65 @@
+// Host-side launchers of the miclip CDNA4 kernels (internal interface).
+// Every launcher validates the shapes its kernel assumes and returns
+// hipErrorInvalidValue instead of launching when they do not hold.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace miclip {
+
+enum Act { ACT_NONE = 0, ACT_QUICKGELU = 1, ACT_GELU = 2 };
+
+// ---- GEMM: C[M,N] = A[M,K] . W[N,K]^T (+ epilogue); A, W in compute dtype ----
+// Shapes: N % 128 == 0, K % 64 == 0, any M >= 1; A, W rows K-contiguous.
+// Store epilogue: C (compute dtype, ld = N) = act(acc + bias).
+hipError_t gemm_store(int dtype, const void* A, const void* W, const float* bias, void* C,
+                      int M, int N, int K, int act, hipStream_t s);
+// Residual epilogue: X (fp32, ld = N) += acc + bias.
+hipError_t gemm_residual(int dtype, const void* A, const void* W, const float* bias, float* X,
+                         int M, int N, int K, hipStream_t s);
+// Float epilogue: C (fp32, ld = N) = acc + bias (bias may be null).
+hipError_t gemm_f32(int dtype, const void* A, const void* W, const float* bias, float* C,
+                    int M, int N, int K, hipStream_t s);
+// Patch-embed epilogue: row m = b*np + p of the patch GEMM goes to token row
+// b*(np+1) + 1 + p of X (fp32, ld = N), plus positional embedding row 1 + p.
+hipError_t gemm_patch(int dtype, const void* A, const void* W, const float* pos, float* X,
+                      int M, int N, int K, int np, hipStream_t s);
+
+// ---- LayerNorm (fp32 statistics, eps 1e-5) over rows of width D ----
+// Row r of the input is at in + in_row(r)*D with in_row(r) = rows ? rows[r] : r*in_stride_rows.
+// out_f32 != null -> fp32 output (may alias in); else out_t in compute dtype.
+// normalize != 0 additionally L2-normalises each output row (F.normalize, eps 1e-12).
+hipError_t layernorm(int dtype, const float* in, const int32_t* rows, int in_stride_rows,
+                     const float* gamma, const float* beta, float* out_f32, void* out_t,
+                     int R, int D, int normalize, hipStream_t s);
+
+// ---- fused multi-head attention over a packed QKV buffer ----
+// qkv: [B*N, 3*H*64] compute dtype (torch in_proj order q|k|v); out: [B*N, H*64].
+// head dim 64; causal adds the -inf strictly-upper-triangular mask (clip/model.py:323-329).
+hipError_t attention(int dtype, const void* qkv, void* out, int B, int N, int H, int causal,
+                     hipStream_t s);
+
+// ---- embeddings / gathers ----
+// images fp32 [B,3,R,R] -> patches [B*g*g, Kp] compute dtype, col = c*P*P + ky*P + kx,
+// zero-padded up to Kp (multiple of 64).
+hipError_t im2col(int dtype, const float* img, void* patches, int B, int R, int P, int Kp,
+                  hipStream_t s);
+// X[b*ntok + 0, :] = cls + pos[0, :]
+hipError_t class_token(const float* cls, const float* pos, float* X, int B, int ntok, int D,
+                       hipStream_t s);
+// X[p*L + t, :] = tok_emb[tokens[p*L + t], :] + pos[t, :]; eot[p] = argmax_t tokens[p*L+t]
+// as a row index p*L + argmax (first maximum, like torch.argmax).
+hipError_t token_embed(const int64_t* tokens, const float* tok_emb, const float* pos, float* X,
+                       int32_t* eot_rows, int P, int L, int D, int vocab, hipStream_t s);
+// out[r, :] = in[r, :] @ Wm  (fp32, Wm [D, E] row-major)
+hipError_t rowvec_matmul(const float* in, const float* Wm, float* out, int R, int D, int E,
+                         hipStream_t s);
+// in-place row L2 normalisation (F.normalize, eps 1e-12), fp32 [R, D]
+hipError_t row_l2norm(float* x, int R, int D, hipStream_t s);
+// zero-shot head: f = normalize(x @ proj) (proj may be null -> f = normalize(x));
+// logits = scale * f @ tw ([E, C]); topk indices (sorted, largest first).
+hipError_t zero_shot(const float* x, const float* proj, const float* tw, float* logits,
+                     int32_t* topk, int B, int Din, int E, int C, float scale, int k,
+                     hipStream_t s);
+
+}  // namespace miclip

@@ -1,0 +1,101 @@
+"""ctypes binding of libmiclip.so (the C ABI declared in include/miclip.h).
+
+The product path has no fallback: if the HIP library is missing or cannot be
+loaded, every entry point raises. Build it with `make` (or
+`python -c "import __graft_entry__ as g; g.build()"`).
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MICLIP_LIB", os.path.join(_HERE, "libmiclip.so"))
+
+MICLIP_FP16 = 0
+MICLIP_BF16 = 1
+MICLIP_ACT_QUICKGELU = 1
+MICLIP_ACT_GELU = 2
+MICLIP_FLAG_NORMALIZE = 1
+MICLIP_FLAG_APPLY_PROJ = 2
+
+EXPORTS = (
+    "miclip_model_create", "miclip_model_load_weights", "miclip_reserve",
+    "miclip_encode_image", "miclip_encode_text", "miclip_zero_shot",
+    "miclip_model_destroy", "miclip_last_error", "miclip_abi_version",
+    "miclip_model_bytes", "miclip_set_profiling", "miclip_profile_read",
+    "miclip_op_gemm", "miclip_op_layernorm", "miclip_op_attention",
+)
+
+
+class MiclipConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "embed_dim", "image_resolution", "vision_layers", "vision_width", "vision_patch_size",
+        "context_length", "vocab_size", "transformer_width", "transformer_heads",
+        "transformer_layers", "compute_dtype", "act")]
+
+
+class MiclipTensor(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("data", ctypes.c_void_p), ("numel", ctypes.c_int64)]
+
+
+class MiclipKernelStat(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("launches", ctypes.c_int64), ("ms", ctypes.c_double),
+                ("flops", ctypes.c_double), ("bytes", ctypes.c_double)]
+
+
+class MiclipError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load_library(path: str = None):
+    """Load (once) and return the ctypes handle; raises MiclipError if absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.isfile(p):
+        raise MiclipError(f"HIP library not found at {p}; build it with `make` "
+                          f"(miclip has no CPU fallback)")
+    lib = ctypes.CDLL(p)
+    vp, i32, i64, u32, f32 = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
+                              ctypes.c_float)
+    sig = {
+        "miclip_model_create": ([ctypes.POINTER(MiclipConfig), ctypes.c_int, ctypes.POINTER(vp)], ctypes.c_int),
+        "miclip_model_load_weights": ([vp, ctypes.POINTER(MiclipTensor), i32], ctypes.c_int),
+        "miclip_reserve": ([vp, i32, i32], ctypes.c_int),
+        "miclip_encode_image": ([vp, vp, i32, vp, u32, vp], ctypes.c_int),
+        "miclip_encode_text": ([vp, vp, i32, vp, vp, vp], ctypes.c_int),
+        "miclip_zero_shot": ([vp, vp, i32, i32, vp, i32, f32, vp, vp, i32, vp], ctypes.c_int),
+        "miclip_model_destroy": ([vp], None),
+        "miclip_last_error": ([], ctypes.c_char_p),
+        "miclip_abi_version": ([], ctypes.c_int),
+        "miclip_model_bytes": ([vp], i64),
+        "miclip_set_profiling": ([vp, ctypes.c_int], ctypes.c_int),
+        "miclip_profile_read": ([vp, ctypes.POINTER(MiclipKernelStat), i32, i32], ctypes.c_int),
+        "miclip_op_gemm": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp], ctypes.c_int),
+        "miclip_op_layernorm": ([i32, vp, vp, vp, vp, i32, i32, i32, vp], ctypes.c_int),
+        "miclip_op_attention": ([i32, vp, vp, i32, i32, i32, i32, vp], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = load_library().miclip_last_error().decode(errors="replace")
+        exc = ValueError if rc == -1 else MiclipError
+        raise exc(f"{what} failed ({rc}): {msg}")
+    return rc
+
+
+def stream_handle(device=None):
+    """Raw hipStream_t of torch's current stream on `device`."""
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,286 @@
+"""`CLIP` nn.Module whose encoders run on the HIP C ABI (libmiclip.so).
+
+Drop-in for the object the reference's `clip.load` returns (clip/model.py:238-369
+built by build_model, clip/model.py:396-433). What callers of the reference
+touch, and how it is honoured here:
+
+  * `parameters()` / `named_parameters()` / `state_dict()`: real fp32 torch
+    Parameters on the HIP device, named exactly as CLIP.state_dict(), so device
+    inference (methods/utils.py:151-153, utils.py:33,
+    aihab_utils/feature_cache.py:191) and `state_dict()["visual.proj"]`
+    (methods/ProLIP.py:89) work unchanged;
+  * `visual.input_resolution`, `visual.output_dim`, `visual.proj`,
+    `visual.conv1.weight`, `context_length`, `vocab_size`, `dtype`;
+  * `encode_image(image) -> Tensor[B, vision_width]` (pre-projection,
+    clip/model.py:228-235) and `encode_text(text) -> (x_before, x)`
+    (clip/model.py:338-353). Outputs are fresh, writable fp32 tensors (callers
+    divide them in place, utils.py:46-48).
+
+The encoders never run in PyTorch: they call the C ABI, which fails loudly if
+the library or the device is missing. The Parameters are the source of truth
+for `state_dict`; the handle holds repacked device copies (GEMM weights in the
+compute dtype) that are rebuilt whenever the module moves to another device.
+"""
+import ctypes
+import warnings
+
+import numpy as np
+import torch
+from torch import nn
+
+from . import _lib
+from .configs import CLIPConfig
+
+_DTYPES = {"fp16": (_lib.MICLIP_FP16, torch.float16), "float16": (_lib.MICLIP_FP16, torch.float16),
+           "bf16": (_lib.MICLIP_BF16, torch.bfloat16), "bfloat16": (_lib.MICLIP_BF16, torch.bfloat16)}
+
+
+class _Node(nn.Module):
+    """Container mirroring one level of the reference module tree."""
+
+
+class _Handle:
+    """Owns one miclip_model* (device-bound)."""
+
+    def __init__(self, cfg: CLIPConfig, compute_dtype: int, device_index: int):
+        self.lib = _lib.load_library()
+        c = _lib.MiclipConfig(
+            embed_dim=cfg.embed_dim, image_resolution=cfg.image_resolution,
+            vision_layers=cfg.vision_layers, vision_width=cfg.vision_width,
+            vision_patch_size=cfg.vision_patch_size, context_length=cfg.context_length,
+            vocab_size=cfg.vocab_size, transformer_width=cfg.transformer_width,
+            transformer_heads=cfg.transformer_heads, transformer_layers=cfg.transformer_layers,
+            compute_dtype=compute_dtype,
+            act=_lib.MICLIP_ACT_GELU if cfg.act == "erf" else _lib.MICLIP_ACT_QUICKGELU)
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.miclip_model_create(ctypes.byref(c), device_index, ctypes.byref(h)),
+                   "miclip_model_create")
+        self.ptr = h
+        self.device_index = device_index
+
+    def load(self, named_arrays):
+        keep = []
+        arr = (_lib.MiclipTensor * len(named_arrays))()
+        for i, (name, a) in enumerate(named_arrays):
+            a = np.ascontiguousarray(a, dtype=np.float32)
+            keep.append(a)
+            arr[i].name = name.encode()
+            arr[i].data = a.ctypes.data
+            arr[i].numel = a.size
+        _lib.check(self.lib.miclip_model_load_weights(self.ptr, arr, len(named_arrays)),
+                   "miclip_model_load_weights")
+
+    def close(self):
+        if self.ptr:
+            self.lib.miclip_model_destroy(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class CLIP(nn.Module):
+    def __init__(self, cfg: CLIPConfig, state_dict, device="cuda", compute_dtype="fp16"):
+        super().__init__()
+        if compute_dtype not in _DTYPES:
+            raise ValueError(f"compute_dtype must be one of {sorted(_DTYPES)}")
+        self.config = cfg
+        self.compute_dtype = compute_dtype
+        self.context_length = cfg.context_length
+        self.vocab_size = cfg.vocab_size
+        dev = torch.device(device)
+        if dev.type != "cuda":
+            raise RuntimeError("miclip encoders run on a HIP device only (got device "
+                               f"{dev}); there is no CPU path")
+        if not torch.cuda.is_available():
+            raise RuntimeError("miclip needs a HIP (ROCm) device; torch.cuda.is_available() is False")
+        for name, value in state_dict.items():
+            t = value if isinstance(value, torch.Tensor) else torch.from_numpy(np.asarray(value))
+            self._register(name, nn.Parameter(t.detach().to(torch.float32).clone(), requires_grad=False))
+        self.visual.input_resolution = cfg.image_resolution
+        self.visual.output_dim = cfg.embed_dim
+        self._handle = None
+        self.to(dev)
+
+    # -- module tree -------------------------------------------------------
+    def _register(self, dotted, param):
+        parts = dotted.split(".")
+        mod = self
+        for p in parts[:-1]:
+            if not hasattr(mod, p) or not isinstance(getattr(mod, p), nn.Module):
+                mod.add_module(p, _Node())
+            mod = getattr(mod, p)
+        mod.register_parameter(parts[-1], param)
+
+    def _apply(self, fn, recurse=True):
+        out = super()._apply(fn, recurse)
+        self._sync_handle()
+        return out
+
+    def _sync_handle(self):
+        p = self.visual.conv1.weight
+        if p.device.type != "cuda":
+            if self._handle is not None:
+                self._handle.close()
+            self._handle = None
+            return
+        idx = p.device.index if p.device.index is not None else torch.cuda.current_device()
+        if self._handle is not None and self._handle.device_index == idx:
+            return
+        if self._handle is not None:
+            self._handle.close()
+        h = _Handle(self.config, _DTYPES[self.compute_dtype][0], idx)
+        h.load([(k, v.detach().float().cpu().numpy()) for k, v in self.state_dict().items()])
+        self._handle = h
+
+    def refresh_weights(self):
+        """Re-upload Parameters after they were modified in place."""
+        if self._handle is not None:
+            self._handle.load([(k, v.detach().float().cpu().numpy())
+                               for k, v in self.state_dict().items()])
+
+    # -- reference surface ---------------------------------------------------
+    @property
+    def dtype(self):
+        # clip/model.py:331-333 returns conv1.weight.dtype, the GPU compute dtype
+        return _DTYPES[self.compute_dtype][1]
+
+    @property
+    def device(self):
+        return self.visual.conv1.weight.device
+
+    def _require(self):
+        if self._handle is None:
+            raise RuntimeError("model is not on a HIP device; call .cuda() / .to('cuda')")
+        return self._handle
+
+    def reserve(self, max_images=0, max_prompts=0):
+        h = self._require()
+        _lib.check(h.lib.miclip_reserve(h.ptr, int(max_images), int(max_prompts)), "miclip_reserve")
+
+    def set_profiling(self, enable=True):
+        h = self._require()
+        _lib.check(h.lib.miclip_set_profiling(h.ptr, int(bool(enable))), "miclip_set_profiling")
+
+    def profile_read(self, reset=True):
+        """{kernel class: dict(launches, ms, flops, bytes)} from the HIP-event profiler."""
+        h = self._require()
+        arr = (_lib.MiclipKernelStat * 32)()
+        n = h.lib.miclip_profile_read(h.ptr, arr, 32, int(bool(reset)))
+        if n < 0:
+            _lib.check(n, "miclip_profile_read")
+        return {arr[i].name.decode(): dict(launches=arr[i].launches, ms=arr[i].ms,
+                                           flops=arr[i].flops, bytes=arr[i].bytes)
+                for i in range(n) if arr[i].launches}
+
+    @torch.no_grad()
+    def encode_image(self, image, normalize=False, apply_proj=False, out=None):
+        """Pre-projection image features [B, vision_width] (clip/model.py:335-336, 216-235).
+
+        normalize / apply_proj fuse the callers' F.normalize
+        (aihab_utils/feature_cache.py:126-127) and `@ visual.proj`
+        (methods/ProLIP.py:38-41) into the same launch sequence.
+        """
+        h = self._require()
+        if image.dim() != 4 or image.shape[1] != 3 or image.shape[2] != image.shape[3] \
+                or image.shape[2] != self.config.image_resolution:
+            raise ValueError(f"expected images [B, 3, {self.config.image_resolution}, "
+                             f"{self.config.image_resolution}], got {tuple(image.shape)}")
+        img = image.to(device=self.device, dtype=torch.float32).contiguous()
+        B = img.shape[0]
+        dim = self.config.embed_dim if apply_proj else self.config.vision_width
+        if out is None:
+            out = torch.empty(B, dim, device=self.device, dtype=torch.float32)
+        elif out.shape != (B, dim) or out.dtype != torch.float32 or not out.is_contiguous():
+            raise ValueError("out must be a contiguous float32 tensor of shape "
+                             f"({B}, {dim})")
+        if B == 0:
+            return out
+        flags = (_lib.MICLIP_FLAG_NORMALIZE if normalize else 0) | \
+                (_lib.MICLIP_FLAG_APPLY_PROJ if apply_proj else 0)
+        with torch.cuda.device(self.device):
+            _lib.check(h.lib.miclip_encode_image(h.ptr, img.data_ptr(), B, out.data_ptr(), flags,
+                                                 _lib.stream_handle(self.device)),
+                       "miclip_encode_image")
+        return out
+
+    @torch.no_grad()
+    def encode_text(self, text):
+        """(x_before_proj [P, transformer_width], x [P, embed_dim]) (clip/model.py:338-353)."""
+        h = self._require()
+        if text.dim() != 2 or text.shape[1] != self.context_length:
+            raise ValueError(f"expected tokens [P, {self.context_length}], got {tuple(text.shape)}")
+        if text.device.type == "cpu":
+            if text.numel() and (int(text.min()) < 0 or int(text.max()) >= self.vocab_size):
+                raise IndexError("index out of range in self (token id outside the vocabulary)")
+        tok = text.to(device=self.device, dtype=torch.int64).contiguous()
+        P = tok.shape[0]
+        xb = torch.empty(P, self.config.transformer_width, device=self.device, dtype=torch.float32)
+        xp = torch.empty(P, self.config.embed_dim, device=self.device, dtype=torch.float32)
+        if P == 0:
+            return xb, xp
+        with torch.cuda.device(self.device):
+            _lib.check(h.lib.miclip_encode_text(h.ptr, tok.data_ptr(), P, xb.data_ptr(),
+                                                xp.data_ptr(), _lib.stream_handle(self.device)),
+                       "miclip_encode_text")
+        return xb, xp
+
+    @torch.no_grad()
+    def zero_shot(self, feats, text_weights, scale=100.0, k=1, apply_proj=True):
+        """logits = scale * normalize(feats [@ visual.proj]) @ text_weights and top-k indices.
+
+        methods/ProLIP.py:38-41 + 288-293 (scale 100), methods/utils.py:16-21 (topk).
+        """
+        h = self._require()
+        f = feats.to(device=self.device, dtype=torch.float32).contiguous()
+        tw = text_weights.to(device=self.device, dtype=torch.float32).contiguous()
+        B, C = f.shape[0], tw.shape[1]
+        din = self.config.vision_width if apply_proj else self.config.embed_dim
+        if f.dim() != 2 or f.shape[1] != din or tw.shape[0] != self.config.embed_dim:
+            raise ValueError(f"feats must be [B, {din}] and text_weights [{self.config.embed_dim}, C]")
+        if not 0 <= k <= C:
+            raise ValueError(f"k must be in [0, {C}]")
+        logits = torch.empty(B, C, device=self.device, dtype=torch.float32)
+        top = torch.empty(B, max(k, 1), device=self.device, dtype=torch.int32)
+        if B:
+            with torch.cuda.device(self.device):
+                _lib.check(h.lib.miclip_zero_shot(h.ptr, f.data_ptr(), B, int(bool(apply_proj)),
+                                                  tw.data_ptr(), C, float(scale), logits.data_ptr(),
+                                                  top.data_ptr() if k else None, int(k),
+                                                  _lib.stream_handle(self.device)),
+                           "miclip_zero_shot")
+        return logits, top[:, :k].long()
+
+    def forward(self, image, text):
+        """Upstream CLIP.forward semantics (clip/model.py:355-369) on the joint embedding.
+
+        The vendored forward raises (encode_text returns a tuple);
+        this one computes what it was meant to: cosine logits with logit_scale.exp().
+        """
+        img = self.encode_image(image, normalize=True, apply_proj=True)
+        _, txt = self.encode_text(text)
+        txt = txt / txt.norm(dim=-1, keepdim=True)
+        logits_per_image = self.logit_scale.exp() * img @ txt.t()
+        return logits_per_image, logits_per_image.t()
+
+    def extra_repr(self):
+        c = self.config
+        return (f"vision=ViT(W={c.vision_width}, L={c.vision_layers}, P={c.vision_patch_size}, "
+                f"R={c.image_resolution}), text=(W={c.transformer_width}, L={c.transformer_layers}), "
+                f"embed_dim={c.embed_dim}, compute_dtype={self.compute_dtype}")
+
+
+def build_model(state_dict, device="cuda", compute_dtype="fp16") -> CLIP:
+    """Counterpart of reference build_model (clip/model.py:396-433), ViT only."""
+    from .configs import config_from_state_dict
+    sd = dict(state_dict)
+    for key in ("input_resolution", "context_length", "vocab_size"):
+        sd.pop(key, None)
+    cfg = config_from_state_dict(sd)
+    if "logit_scale" not in sd:
+        warnings.warn("state_dict has no logit_scale; using log(1/0.07)")
+        sd["logit_scale"] = torch.tensor(float(np.log(1 / 0.07)))
+    return CLIP(cfg, sd, device=device, compute_dtype=compute_dtype).eval()

@@ -1,0 +1,163 @@
+/*
+ * miclip.h -- C ABI of the MI355X-native CLIP encode path (libmiclip.so).
+ *
+ * The reference (WhiteGiveFive/aihab-clip) is pure Python and has no FFI; its
+ * hot path is the PyTorch call chain behind `clip.load` / `model.encode_image`
+ * / `model.encode_text` and the zero-shot head. Each entry point below states
+ * the reference interface it replaces (paths relative to the reference repo).
+ *
+ * Conventions
+ *   - Plain pointers and sizes only. Image/token/feature/logit buffers are
+ *     caller-owned DEVICE pointers on the handle's device (e.g. torch tensors'
+ *     data_ptr()); weights and workspaces are handle-owned.
+ *   - Every call is stream-ordered on the caller's `stream` (a hipStream_t;
+ *     NULL = the legacy default stream). No call synchronises the device,
+ *     except miclip_model_load_weights / miclip_reserve, which allocate.
+ *   - Return value: 0 on success, a negative MICLIP_E* code on failure; the
+ *     message is available from miclip_last_error() (thread-local).
+ *   - A handle is bound to one device and is not safe for concurrent calls
+ *     from several host threads.
+ */
+#ifndef MICLIP_H_
+#define MICLIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MICLIP_ABI_VERSION 1
+
+enum miclip_status {
+  MICLIP_OK = 0,
+  MICLIP_EINVAL = -1,   /* bad argument / shape (reference raises ValueError / RuntimeError) */
+  MICLIP_EHIP = -2,     /* HIP runtime error */
+  MICLIP_ENOWEIGHTS = -3, /* a tower's weights were not loaded */
+  MICLIP_ENOMEM = -4
+};
+
+enum miclip_dtype { MICLIP_FP16 = 0, MICLIP_BF16 = 1 };
+enum miclip_act { MICLIP_ACT_QUICKGELU = 1, MICLIP_ACT_GELU = 2 };
+
+/* encode_image flags */
+#define MICLIP_FLAG_NORMALIZE 1u  /* F.normalize(feats, dim=-1): aihab_utils/feature_cache.py:126-127 */
+#define MICLIP_FLAG_APPLY_PROJ 2u /* feats @ visual.proj:       methods/ProLIP.py:38-41 */
+
+/* Model hyper-parameters; the fields of clip/model.py:240-254 (CLIP.__init__),
+ * as inferred by build_model (clip/model.py:396-419). ViT towers only. */
+typedef struct miclip_config {
+  int32_t embed_dim;
+  int32_t image_resolution;
+  int32_t vision_layers;
+  int32_t vision_width;
+  int32_t vision_patch_size;
+  int32_t context_length;
+  int32_t vocab_size;
+  int32_t transformer_width;
+  int32_t transformer_heads;
+  int32_t transformer_layers;
+  int32_t compute_dtype; /* miclip_dtype: GEMM/attention operand type (fp32 accumulate) */
+  int32_t act;           /* miclip_act: QuickGELU (clip/model.py:160-162) or exact GELU */
+} miclip_config;
+
+/* One host fp32 tensor of a CLIP state dict, named as in CLIP.state_dict(). */
+typedef struct miclip_tensor {
+  const char* name;
+  const float* data; /* host, contiguous fp32 */
+  int64_t numel;
+} miclip_tensor;
+
+typedef struct miclip_model miclip_model;
+
+/* Replaces the construction half of clip.load (clip/clip.py:89-137) /
+ * build_model (clip/model.py:396-433): creates an empty model on `device`. */
+int miclip_model_create(const miclip_config* cfg, int device, miclip_model** out);
+
+/* Replaces model.load_state_dict + convert_weights (clip/model.py:372-393, 432):
+ * copies/repacks the named tensors into handle-owned device memory (GEMM
+ * weights in the compute dtype, LayerNorm/bias/embeddings fp32). May be called
+ * several times; unknown names are an error, "logit_scale" is accepted and unused. */
+int miclip_model_load_weights(miclip_model* m, const miclip_tensor* tensors, int32_t n);
+
+/* Pre-allocates workspaces for up to max_images images / max_prompts prompts,
+ * so later encode calls allocate nothing (required before hipGraph capture). */
+int miclip_reserve(miclip_model* m, int32_t max_images, int32_t max_prompts);
+
+/* Replaces CLIP.encode_image -> VisionTransformer.forward (clip/model.py:335-336,
+ * 216-235). images: device fp32 [B,3,R,R] (CLIP-normalised, clip/clip.py:80).
+ * out: device fp32 [B, vision_width] pre-projection features (the modified
+ * reference returns ln_post(x[:,0,:]) without @proj, clip/model.py:228-235), or
+ * [B, embed_dim] with MICLIP_FLAG_APPLY_PROJ; MICLIP_FLAG_NORMALIZE L2-normalises. */
+int miclip_encode_image(miclip_model* m, const float* images, int32_t B, float* out,
+                        uint32_t flags, void* stream);
+
+/* Replaces CLIP.encode_text (clip/model.py:338-353), which returns the tuple
+ * (x_before_proj [P, transformer_width], x [P, embed_dim]). tokens: device
+ * int64 [P, context_length] as produced by clip.tokenize (clip/clip.py:192-228);
+ * EOT row = first argmax of each row. Either output may be NULL. */
+int miclip_encode_text(miclip_model* m, const int64_t* tokens, int32_t P, float* x_before,
+                       float* x_proj, void* stream);
+
+/* Replaces the zero-shot head of ProLIP eval / compute_image_features_test:
+ * f = F.normalize(feats @ visual.proj) (apply_proj != 0) or F.normalize(feats);
+ * logits = scale * f @ text_weights  (methods/ProLIP.py:38-41, 288-291;
+ * methods/utils.py:181-186; scale 100 in the reference); topk = logits.topk(k)
+ * indices, sorted (methods/utils.py:16-21). feats: device fp32 [B, Din];
+ * text_weights: device fp32 [embed_dim, C] (clip_classifier output, utils.py:54);
+ * logits: device fp32 [B, C]; topk: device int32 [B, k] or NULL. */
+int miclip_zero_shot(miclip_model* m, const float* feats, int32_t B, int32_t apply_proj,
+                     const float* text_weights, int32_t C, float scale, float* logits,
+                     int32_t* topk, int32_t k, void* stream);
+
+void miclip_model_destroy(miclip_model* m);
+const char* miclip_last_error(void);
+int miclip_abi_version(void);
+/* Device-memory bytes currently held by the handle (weights + workspaces). */
+int64_t miclip_model_bytes(const miclip_model* m);
+
+/* ---- diagnostics: per-kernel-class timing with HIP events ---- */
+
+/* Algorithmic totals of one kernel class since the last reset. `flops` counts
+ * 2*M*N*K per GEMM and 4*N^2*64 per attention head; `bytes` is the minimum HBM
+ * traffic (operands read once, outputs written once). */
+typedef struct miclip_kernel_stat {
+  const char* name;
+  int64_t launches;
+  double ms;
+  double flops;
+  double bytes;
+} miclip_kernel_stat;
+
+/* When enabled, every launch of later encode calls is bracketed by hipEvents on
+ * the caller's stream (adds a few us per launch: use outside timed regions). */
+int miclip_set_profiling(miclip_model* m, int enable);
+/* Synchronises on the recorded events, folds them into per-class totals and
+ * copies up to n classes into out; returns the number of classes. */
+int miclip_profile_read(miclip_model* m, miclip_kernel_stat* out, int32_t n, int32_t reset);
+
+/* ---- op-level entry points (kernel parity tests and micro-benchmarks) ---- */
+
+/* C = A[M,K] . W[N,K]^T + bias, A/W in compute dtype `dtype`.
+ * epi 0: C dtype = act(.) with act from `act` (0 none); epi 1: C fp32 += (residual);
+ * epi 2: C fp32 = . ; N % 128 == 0 and K % 64 == 0 required.
+ * Replaces torch Linear (clip/model.py:171-175) and MHA in/out projections. */
+int miclip_op_gemm(int32_t dtype, const void* A, const void* W, const float* bias, void* C,
+                   int32_t M, int32_t N, int32_t K, int32_t epi, int32_t act, void* stream);
+
+/* LayerNorm over R rows of width D (fp32 in, eps 1e-5), out in fp32 (out_is_f32)
+ * or compute dtype; replaces the reference LayerNorm (clip/model.py:151-157). */
+int miclip_op_layernorm(int32_t dtype, const float* in, const float* gamma, const float* beta,
+                        void* out, int32_t out_is_f32, int32_t R, int32_t D, void* stream);
+
+/* softmax(Q K^T / 8 + mask) V per head over a packed qkv [B*N, 3*H*64] buffer,
+ * out [B*N, H*64]; replaces F.scaled_dot_product_attention inside
+ * nn.MultiheadAttention (clip/model.py:179-181), causal = text mask (323-329). */
+int miclip_op_attention(int32_t dtype, const void* qkv, void* out, int32_t B, int32_t N,
+                        int32_t H, int32_t causal, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MICLIP_H_ */

@@ -1,0 +1,172 @@
+"""Generate tests/golden/*.npz by running the REFERENCE clip/model.py on CPU.
+
+Run in the build container only (needs /root/reference; the GPU box has none):
+
+    PYTHONDONTWRITEBYTECODE=1 python oracle/make_golden.py
+
+What it does, per config:
+  1. draws the seeded weights of `miclip.weights` and feeds them through the
+     reference `build_model` (clip/model.py:396-433) followed by `.float()`,
+     exactly what `clip.load(path, device="cpu")` does (clip/clip.py:133-137);
+  2. encodes seeded synthetic images with the reference `encode_image`
+     (clip/model.py:335) and token-id prompts with `encode_text` (338-353);
+  3. builds class text weights the way `clip_classifier` does (utils.py:31-57)
+     and zero-shot logits the way ProLIP eval does (methods/ProLIP.py:288-293);
+  4. checks that `oracle/clip_oracle.py` reproduces every output (bit-exact
+     is expected; the max abs diff is recorded in the fixture);
+  5. saves inputs' checksums + outputs as a small .npz fixture.
+
+Token ids come from the reference BPE tokenizer (clip/simple_tokenizer.py)
+with a harness-only `ftfy` stub (fix_text = identity: exact for the ASCII
+prompts used) and the `tokenize` padding rule of clip/clip.py:192-228. The
+prompts are the CS class prompts of data/templates.py (CS_TEMPLATES and
+gen_prompts(True, True)).
+
+Nothing from the reference is copied into the repository: only the numeric
+outputs (and the prompt strings they were computed from) are stored.
+"""
+import importlib.util
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = os.environ.get("MICLIP_REFERENCE", "/root/reference")
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.dont_write_bytecode = True
+sys.path.insert(0, os.path.join(ROOT, "aihab-clip_amd"))
+sys.path.insert(0, ROOT)
+
+from miclip.configs import MODEL_CONFIGS  # noqa: E402
+from miclip.weights import generate_state_dict, synthetic_images, checksum  # noqa: E402
+from oracle import clip_oracle  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden")
+
+
+def _load(name, path, package_dirs=None):
+    spec = importlib.util.spec_from_file_location(name, path, submodule_search_locations=package_dirs)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def reference_modules():
+    model = _load("_ref_clip_model", os.path.join(REF, "clip", "model.py"))
+    if "ftfy" not in sys.modules:                     # harness-only stub
+        sys.modules["ftfy"] = types.SimpleNamespace(fix_text=lambda s: s)
+    tok = _load("_ref_simple_tokenizer", os.path.join(REF, "clip", "simple_tokenizer.py"))
+    data = _load("_ref_data", os.path.join(REF, "data", "__init__.py"),
+                 package_dirs=[os.path.join(REF, "data")])
+    templates = _load("_ref_data.templates", os.path.join(REF, "data", "templates.py"))
+    return model, tok, data, templates
+
+
+def tokenize(tokenizer, texts, context_length=77):
+    # restates clip/clip.py:192-228 (no truncation; raise if too long)
+    sot = tokenizer.encoder["<|startoftext|>"]
+    eot = tokenizer.encoder["<|endoftext|>"]
+    out = np.zeros((len(texts), context_length), dtype=np.int32)
+    for i, t in enumerate(texts):
+        ids = [sot] + tokenizer.encode(t) + [eot]
+        if len(ids) > context_length:
+            raise RuntimeError(f"Input {t} is too long for context length {context_length}")
+        out[i, :len(ids)] = ids
+    return out
+
+
+def reference_model(refmodel, sd_np):
+    sd = {k: torch.from_numpy(v.copy()) for k, v in sd_np.items()}
+    m = refmodel.build_model(sd)          # fp16 convert + load_state_dict + eval
+    return m.float()                       # clip/clip.py:135-136 (CPU path)
+
+
+def run_config(tag, model_name, n_images, prompts, refs, seed=0):
+    refmodel, tok_mod, _, _ = refs
+    cfg = MODEL_CONFIGS[model_name]
+    sd = generate_state_dict(cfg, seed=seed)
+    model = reference_model(refmodel, sd)
+    tokenizer = tok_mod.SimpleTokenizer()
+    tokens = tokenize(tokenizer, prompts)
+    imgs = synthetic_images(n_images, cfg.image_resolution, seed=seed)
+
+    torch.set_num_threads(max(1, os.cpu_count() or 1))
+    with torch.no_grad():
+        ref_img = model.encode_image(torch.from_numpy(imgs))
+        ref_before, ref_txt = model.encode_text(torch.from_numpy(tokens).long())
+        # clip_classifier (utils.py:31-57): one encode_text call per class
+        # (one template per class: CS_TEMPLATES / gen_prompts have one entry)
+        ws = []
+        for t in tokens:
+            _, emb = model.encode_text(torch.from_numpy(t[None]).long())
+            emb /= emb.norm(dim=-1, keepdim=True)
+            e = emb.mean(dim=0)
+            e /= e.norm()
+            ws.append(e)
+        tw = torch.stack(ws, dim=1)                                    # [E, C]
+        logits = clip_oracle.zero_shot_logits(ref_img, sd["visual.proj"], tw)
+
+    # oracle restatement against the reference
+    o_img = clip_oracle.encode_image(sd, cfg, imgs)
+    o_before, o_txt = clip_oracle.encode_text(sd, cfg, tokens)
+    o_tw = clip_oracle.class_text_weights(sd, cfg, [t[None] for t in tokens])
+    o_logits = clip_oracle.zero_shot_logits(o_img, sd["visual.proj"], o_tw)
+    diffs = {
+        "encode_image": float((o_img - ref_img).abs().max()),
+        "text_before": float((o_before - ref_before).abs().max()),
+        "text_proj": float((o_txt - ref_txt).abs().max()),
+        "text_weights": float((o_tw - tw).abs().max()),
+        "logits": float((o_logits - logits).abs().max()),
+    }
+    k = min(5, logits.shape[1])
+    fixture = dict(
+        image=ref_img.numpy().astype(np.float32),
+        text_before=ref_before.numpy().astype(np.float32),
+        text_proj=ref_txt.numpy().astype(np.float32),
+        text_weights=tw.numpy().astype(np.float32),
+        logits=logits.numpy().astype(np.float32),
+        topk=clip_oracle.topk(logits, k).numpy().astype(np.int64),
+        margins=clip_oracle.margins(logits).numpy().astype(np.float32),
+        tokens=tokens,
+        meta=np.frombuffer(json.dumps(dict(
+            tag=tag, model=model_name, seed=seed, n_images=n_images,
+            image_crc=checksum(imgs),
+            weight_crc={n: checksum(sd[n]) for n in (
+                "visual.conv1.weight", "visual.proj", "token_embedding.weight",
+                "visual.transformer.resblocks.0.attn.in_proj_weight")},
+            prompts=list(prompts), oracle_vs_reference_maxabs=diffs,
+            torch=torch.__version__, numpy=np.__version__,
+        )).encode(), dtype=np.uint8),
+    )
+    path = os.path.join(OUT, f"{tag}.npz")
+    np.savez_compressed(path, **fixture)
+    print(f"[golden] {tag}: {path} oracle-vs-reference max|d| = {diffs}")
+    return diffs
+
+
+def main():
+    refs = reference_modules()
+    _, _, data, templates = refs
+    os.makedirs(OUT, exist_ok=True)
+    classnames = [c.replace("_", " ") for c in templates.CS_CLASSNAMES]
+    flat = [templates.CS_TEMPLATES[0].format(c) for c in classnames]   # utils.py:40-41
+    import contextlib, io
+    with contextlib.redirect_stdout(io.StringIO()):
+        hier, _ = templates.gen_prompts(True, True)                    # data/templates.py:236
+    c1_prompts = flat[:10]
+    all_diffs = {}
+    all_diffs["vitb32"] = run_config("vitb32", "ViT-B/32", 8, c1_prompts, refs)
+    all_diffs["vitb16"] = run_config("vitb16", "ViT-B/16", 4, flat, refs)
+    all_diffs["vitl14"] = run_config("vitl14", "ViT-L/14", 4, hier, refs)
+    all_diffs["vitl14_336"] = run_config("vitl14_336", "ViT-L/14@336px", 2, hier, refs)
+    worst = max(max(d.values()) for d in all_diffs.values())
+    print(f"[golden] worst oracle-vs-reference max|d| over all outputs: {worst:.3e}")
+
+
+if __name__ == "__main__":
+    main()

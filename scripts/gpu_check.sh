@@ -1,0 +1,27 @@
+#!/bin/bash
+# GPU-box check sequence: each step has its own time limit; a crash, abort or
+# timeout (any status other than 0 or pytest's 1 = "tests failed") stops the run.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+run() {
+  local name=$1 limit=$2; shift 2
+  echo "=== $name: $*"
+  timeout -k 10 "$limit" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"; tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+}
+steps=("$@")
+[ ${#steps[@]} -eq 0 ] && steps=(kernels parity bench)
+for step in "${steps[@]}"; do
+  case $step in
+    kernels) run kernels 400 python -m pytest tests/test_gpu_kernels.py -q -rf ;;
+    parity)  run parity 900 python -m pytest tests/test_gpu_parity.py -q -s -rf ;;
+    gpu)     run gputests 1000 python -m pytest tests -m gpu -q -rf ;;
+    smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)   run bench 600 python bench.py --steps 10 --warmup 3 ;;
+    benchq)  run benchq 400 python bench.py --steps 5 --warmup 2 --cpu-seconds 5 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done

@@ -1,0 +1,125 @@
+"""Kernel-level parity of the HIP path (through the C ABI) against torch fp32.
+
+Each test feeds the same rounded (fp16/bf16) operands to the kernel and to a
+plain fp32 torch reference of the same op, and bounds the difference.
+"""
+import ctypes
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DT = {"fp16": (0, torch.float16), "bf16": (1, torch.bfloat16)}
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from miclip import _lib
+    return _lib.load_library()
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _check(lib, rc):
+    assert rc == 0, lib.miclip_last_error().decode()
+
+
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+@pytest.mark.parametrize("M,N,K", [(300, 256, 192), (128, 128, 64), (65, 384, 1024), (1000, 768, 3072)])
+@pytest.mark.parametrize("epi,act", [(0, 0), (0, 1), (0, 2), (1, 0), (2, 0)])
+def test_gemm(lib, dt, M, N, K, epi, act):
+    code, tdt = DT[dt]
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K + epi * 3 + act)
+    A = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(tdt)
+    W = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).to(tdt)
+    bias = torch.randn(N, device="cuda", generator=g) * 0.1
+    ref = A.float() @ W.float().t() + bias
+    if epi == 0:
+        if act == 1:
+            ref = ref * torch.sigmoid(1.702 * ref)
+        elif act == 2:
+            ref = torch.nn.functional.gelu(ref)
+        C = torch.empty(M, N, device="cuda", dtype=tdt)
+    elif epi == 1:
+        X0 = torch.randn(M, N, device="cuda", generator=g)
+        C = X0.clone()
+        ref = X0 + ref
+    else:
+        C = torch.empty(M, N, device="cuda", dtype=torch.float32)
+    _check(lib, lib.miclip_op_gemm(code, A.data_ptr(), W.data_ptr(), bias.data_ptr(), C.data_ptr(),
+                                   M, N, K, epi, act, _stream()))
+    torch.cuda.synchronize()
+    err = (C.float() - ref).abs().max().item()
+    tol = (2e-2 if dt == "bf16" else 4e-3) * max(1.0, ref.abs().max().item()) if epi == 0 else 2e-4 * K ** 0.5
+    assert err <= tol, f"max|err| {err} > {tol}"
+
+
+def test_gemm_rejects_bad_shapes(lib):
+    A = torch.zeros(16, 64, device="cuda", dtype=torch.float16)
+    W = torch.zeros(100, 64, device="cuda", dtype=torch.float16)
+    C = torch.zeros(16, 100, device="cuda", dtype=torch.float16)
+    rc = lib.miclip_op_gemm(0, A.data_ptr(), W.data_ptr(), None, C.data_ptr(), 16, 100, 64, 0, 0, _stream())
+    assert rc == -1
+
+
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+@pytest.mark.parametrize("R,D", [(7, 768), (513, 1024), (64, 512), (3, 1280)])
+def test_layernorm(lib, dt, R, D):
+    code, tdt = DT[dt]
+    x = torch.randn(R, D, device="cuda") * 3 + 0.5
+    gam = 1 + 0.1 * torch.randn(D, device="cuda")
+    bet = 0.05 * torch.randn(D, device="cuda")
+    ref = torch.nn.functional.layer_norm(x, (D,), gam, bet, 1e-5)
+    out32 = torch.empty(R, D, device="cuda")
+    _check(lib, lib.miclip_op_layernorm(code, x.data_ptr(), gam.data_ptr(), bet.data_ptr(),
+                                        out32.data_ptr(), 1, R, D, _stream()))
+    outt = torch.empty(R, D, device="cuda", dtype=tdt)
+    _check(lib, lib.miclip_op_layernorm(code, x.data_ptr(), gam.data_ptr(), bet.data_ptr(),
+                                        outt.data_ptr(), 0, R, D, _stream()))
+    torch.cuda.synchronize()
+    assert (out32 - ref).abs().max().item() < 1e-4
+    assert (outt.float() - ref).abs().max().item() < (3e-2 if dt == "bf16" else 4e-3)
+
+
+def _attn_ref(qkv, B, N, H, causal):
+    q, k, v = qkv.float().view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    mask = None
+    if causal:
+        mask = torch.full((N, N), float("-inf"), device=qkv.device).triu_(1)
+    o = torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=mask)
+    return o.permute(0, 2, 1, 3).reshape(B * N, H * 64)
+
+
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+@pytest.mark.parametrize("B,N,H,causal", [(2, 50, 3, 0), (3, 77, 2, 1), (2, 257, 2, 0),
+                                          (1, 577, 2, 0), (2, 197, 1, 0), (1, 32, 1, 1),
+                                          (1, 1, 1, 0), (2, 100, 2, 1)])
+def test_attention(lib, dt, B, N, H, causal):
+    code, tdt = DT[dt]
+    g = torch.Generator(device="cuda").manual_seed(B * 1000 + N + H + causal)
+    qkv = (torch.randn(B * N, 3 * H * 64, device="cuda", generator=g) * 1.5).to(tdt)
+    out = torch.empty(B * N, H * 64, device="cuda", dtype=tdt)
+    _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), out.data_ptr(), B, N, H, causal, _stream()))
+    torch.cuda.synchronize()
+    ref = _attn_ref(qkv, B, N, H, causal)
+    err = (out.float() - ref).abs().max().item()
+    assert err < (4e-2 if dt == "bf16" else 6e-3), err
+
+
+def test_attention_spike(lib):
+    """A key row that dominates one query forces the online-softmax rescale branch."""
+    B, N, H = 1, 257, 1
+    qkv = torch.randn(B * N, 3 * 64, device="cuda") * 0.5
+    qkv[100, :64] = 2.0          # query 100
+    qkv[200, 64:128] = 2.0       # key 200 in the 7th key tile -> max jumps late
+    qkv = qkv.half()
+    out = torch.empty(B * N, 64, device="cuda", dtype=torch.float16)
+    _check(lib, lib.miclip_op_attention(0, qkv.data_ptr(), out.data_ptr(), B, N, H, 0, _stream()))
+    torch.cuda.synchronize()
+    ref = _attn_ref(qkv, B, N, H, 0)
+    assert (out.float() - ref).abs().max().item() < 6e-3
