@@ -1,0 +1,264 @@
+"""Batched-encode drivers of the reference, on the HIP encode path.
+
+Counterparts (same names, arguments, outputs, file layout and error behaviour):
+  * compute_image_features        methods/utils.py:142-173
+  * compute_image_features_test   methods/utils.py:175-189
+  * cache_openclip_embeddings     aihab_utils/feature_cache.py:98-186
+  * cache_preprojection_features  aihab_utils/feature_cache.py:189-250
+  * _feature_cache_dir / _embedding_cache_dir / _canonical_backbone_name /
+    _feature_cache_exists          aihab_utils/feature_cache.py:18-65, 253-261
+
+plus the multi-GPU variant the reference does not have:
+  * shard_range / sharded_encode / compute_image_features_sharded: each rank
+    encodes a contiguous slice of the image batch and the L2-normalised (or
+    raw) embeddings are all-gathered over RCCL (torch.distributed backend
+    "nccl" on ROCm) back into the single-GPU row order, so cached
+    embeddings.pt rows still line up with labels.pt / metadata.csv.
+
+Differences that matter to callers: features are fp32 (the reference's GPU
+path returns fp16); the encode itself runs in the C ABI, with the optional
+normalise fused into ln_post.
+"""
+import json
+from datetime import datetime
+from pathlib import Path
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+
+def _canonical_backbone_name(backbone: str) -> str:
+    if not backbone:
+        return "unknown"
+    if backbone == "ViT-B/16":
+        return "ViTB16"
+    if backbone == "ViT-B/32":
+        return "ViTB32"
+    name = backbone.replace("hf-hub:", "hf-hub_")
+    return name.replace("/", "_").replace(" ", "_").replace(":", "_")
+
+
+def _backbone(cfg) -> str:
+    backend = str(cfg.get("clip_backend", "openai")).lower()
+    if backend == "openclip":
+        return cfg.get("open_clip_model", cfg.get("backbone", "RN50"))
+    return cfg.get("backbone", "RN50")
+
+
+def _feature_cache_dir(cfg) -> Path:
+    root = Path(cfg.get("root_path", "./"))
+    shots = int(cfg.get("shots", 0) or 0)
+    seed = int(cfg.get("seed", 1) or 1)
+    return (root / f"features_{_canonical_backbone_name(_backbone(cfg))}_{cfg.get('dataset', 'cs')}"
+            / f"{shots}_shot" / f"seed{seed}")
+
+
+def _embedding_cache_dir(cfg, split: str) -> Path:
+    root = Path(cfg.get("root_path", "./"))
+    ft = cfg.get("finetune", {}) or {}
+    out_root = Path(ft.get("cache_embeddings_dir", "feat_cache_vis"))
+    if not out_root.is_absolute():
+        out_root = root / out_root
+    seed = int(cfg.get("seed", 1) or 1)
+    return (out_root / f"{_canonical_backbone_name(_backbone(cfg))}_{cfg.get('dataset', 'cs')}"
+            / str(split).lower() / f"seed{seed}")
+
+
+def _feature_cache_exists(cache_dir: Path, aug_views: int) -> bool:
+    cache_dir = Path(cache_dir)
+    if not cache_dir.exists() or not (cache_dir / "label.pth").is_file():
+        return False
+    return all((cache_dir / f"f{v}.pth").is_file() for v in range(aug_views))
+
+
+def _model_device(clip_model):
+    try:
+        params = list(clip_model.parameters())
+        return params[0].device if params else torch.device("cuda")
+    except Exception:
+        return torch.device("cuda")
+
+
+@torch.no_grad()
+def compute_image_features(clip_model, loader, to_cpu: bool = False):
+    """Pre-projection features and labels of every batch (methods/utils.py:142-173)."""
+    device = _model_device(clip_model)
+    feats, labels = [], []
+    for images, target in loader:
+        images = images.to(device, non_blocking=True)
+        x = clip_model.encode_image(images)
+        if to_cpu:
+            feats.append(x.detach().to("cpu"))
+            labels.append(target.detach().to("cpu"))
+        else:
+            feats.append(x)
+            labels.append(target.to(device, non_blocking=True))
+    return torch.cat(feats, dim=0), torch.cat(labels, dim=0)
+
+
+@torch.no_grad()
+def compute_image_features_test(clip_model, loader, proj, text_weights):
+    """Top-1 accuracy (%) of the zero-shot head (methods/utils.py:175-189).
+
+    `proj` is the [Wv, E] projection matrix or a callable such as ProLIP's
+    VisProjViT; normalise -> 100 * f @ W -> argmax runs in the HIP head kernel."""
+    device = _model_device(clip_model)
+    hits = []
+    for images, target in loader:
+        x = clip_model.encode_image(images.to(device))
+        f = proj(x) if callable(proj) and not isinstance(proj, torch.Tensor) else x @ proj.to(x)
+        _, top = clip_model.zero_shot(f, text_weights, 100.0, k=1, apply_proj=False)
+        hits += (top[:, 0].cpu() == target.cpu()).tolist()
+    return 100 * float(np.mean(hits))
+
+
+def _to_py(v: Any) -> Any:
+    if isinstance(v, torch.Tensor):
+        return v.item() if v.numel() == 1 else v.detach().cpu().tolist()
+    if isinstance(v, np.generic):
+        return v.item()
+    return v
+
+
+def _metadata_rows(metadata: Any, batch_size: int) -> List[Dict[str, Any]]:
+    if not isinstance(metadata, dict):
+        print("[warn] metadata missing; writing default values in metadata.csv."
+              if metadata is None else
+              "[warn] metadata is not a dict; writing default values in metadata.csv.")
+        return [{} for _ in range(batch_size)]
+    return [{k: _to_py(v[i] if isinstance(v, (list, tuple, np.ndarray, torch.Tensor)) else v)
+             for k, v in metadata.items()} for i in range(batch_size)]
+
+
+@torch.no_grad()
+def cache_openclip_embeddings(cfg: dict, model, loader, split: str = "test",
+                              checkpoint_path: Optional[str] = None) -> Path:
+    """embeddings.pt / labels.pt / metadata.csv / meta.json (aihab_utils/feature_cache.py:98-186)."""
+    import pandas as pd
+    ft = cfg.get("finetune", {}) or {}
+    normalize = bool(ft.get("cache_embeddings_normalize", True))
+    cache_dir = _embedding_cache_dir(cfg, split)
+    cache_dir.mkdir(parents=True, exist_ok=True)
+    device = _model_device(model)
+    model.eval()
+    feats_list, labels_list, rows = [], [], []
+    for batch in loader:
+        if isinstance(batch, (list, tuple)) and len(batch) == 3:
+            images, targets, metadata = batch
+        elif isinstance(batch, (list, tuple)) and len(batch) == 2:
+            images, targets = batch
+            metadata = None
+        else:
+            raise ValueError("Expected batch to be (images, targets) or (images, targets, metadata).")
+        images = images.to(device, non_blocking=True)
+        if hasattr(model, "zero_shot"):          # miclip model: normalise fused into ln_post
+            feats = model.encode_image(images, normalize=normalize)
+        else:
+            feats = model.encode_image(images)
+            if normalize:
+                feats = F.normalize(feats, dim=-1)
+        feats_list.append(feats.detach().to("cpu"))
+        t = targets.detach().to("cpu")
+        labels_list.append(t)
+        for i, row in enumerate(_metadata_rows(metadata, int(t.shape[0]))):
+            rows.append({"file_name": row.get("file_name", ""),
+                         "ground_truth_num_label": int(t[i].item()),
+                         "ground_truth_word_label": row.get("plot_word_label", ""),
+                         "ground_truth_L2_num_label": row.get("l2_label", -1)})
+    feats_all = torch.cat(feats_list, dim=0)
+    labels_all = torch.cat(labels_list, dim=0)
+    torch.save(feats_all, cache_dir / "embeddings.pt")
+    torch.save(labels_all, cache_dir / "labels.pt")
+    cols = ["file_name", "ground_truth_num_label", "ground_truth_word_label",
+            "ground_truth_L2_num_label"]
+    pd.DataFrame(rows).reindex(columns=cols).to_csv(cache_dir / "metadata.csv", index=False)
+    info = {"timestamp": datetime.now().strftime("%Y-%m-%d %H:%M:%S"), "split": str(split),
+            "normalized": normalize, "num_samples": int(feats_all.shape[0]),
+            "dim": int(feats_all.shape[1]) if feats_all.ndim == 2 else None,
+            "checkpoint_path": str(checkpoint_path) if checkpoint_path is not None else None,
+            "cache_dir": str(cache_dir)}
+    with (cache_dir / "meta.json").open("w") as f:
+        json.dump(info, f, indent=2)
+    return cache_dir
+
+
+@torch.no_grad()
+def cache_preprojection_features(cfg, clip_bundle: dict, dl_tr, info: dict):
+    """f{v}.pth per augmentation view + label.pth (aihab_utils/feature_cache.py:189-250)."""
+    clip_model = clip_bundle["clip_model"]
+    cache_dir = _feature_cache_dir(cfg)
+    num_views = int(cfg.get("aug_views", 1) or 1)
+    clip_model.eval()
+    for v in range(num_views):
+        feats_t, labels_t = compute_image_features(clip_model, dl_tr, to_cpu=True)
+        fpath = cache_dir / f"f{v}.pth"
+        fpath.parent.mkdir(parents=True, exist_ok=True)
+        torch.save(feats_t, fpath)
+        if v == 0:
+            torch.save(labels_t, cache_dir / "label.pth")
+        loaded = torch.load(fpath, map_location="cpu", weights_only=True)
+        print({"view": v, "reload_shape_ok": tuple(loaded.shape) == tuple(feats_t.shape),
+               "rows_match_labels": feats_t.shape[0] == labels_t.shape[0]})
+    return cache_dir
+
+
+# ---------------------------------------------------------------- multi-GPU --
+
+def shard_range(n: int, rank: int, world: int):
+    """Contiguous shard [lo, hi) of n items for `rank` (first n % world ranks get one more)."""
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+@torch.no_grad()
+def sharded_encode(encode_fn, images: torch.Tensor, group=None, dim: Optional[int] = None):
+    """Encode this rank's contiguous slice of `images` and all-gather the rows.
+
+    `images` is the full batch (every rank sees the same tensor, e.g. from a
+    deterministic loader) -- only rows shard_range(n, rank, world) are encoded
+    here. Shards are padded to equal length for all_gather_into_tensor and the
+    result is trimmed back, so the output equals encode_fn(images) row for row.
+    Without an initialised process group it degrades to encode_fn(images).
+    """
+    if not (dist.is_available() and dist.is_initialized()):
+        return encode_fn(images)
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    n = images.shape[0]
+    lo, hi = shard_range(n, rank, world)
+    local = encode_fn(images[lo:hi]) if hi > lo else None
+    width = dim if dim is not None else (local.shape[1] if local is not None else None)
+    if width is None:
+        raise ValueError("sharded_encode needs `dim` when a rank has an empty shard")
+    per = -(-n // world)
+    dev = local.device if local is not None else images.device
+    buf = torch.zeros(per, width, device=dev, dtype=torch.float32)
+    if local is not None:
+        buf[: hi - lo] = local
+    out = torch.empty(world * per, width, device=dev, dtype=torch.float32)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    keep = torch.cat([out[r * per: r * per + (shard_range(n, r, world)[1] - shard_range(n, r, world)[0])]
+                      for r in range(world)])
+    return keep
+
+
+@torch.no_grad()
+def compute_image_features_sharded(clip_model, loader, normalize: bool = True, group=None):
+    """compute_image_features over an image-batch-sharded node: every rank walks the
+    same loader, encodes its slice of each batch on its own GPU and receives the
+    all-gathered (normalised) embeddings; returns (features, labels) on the
+    rank's device in the single-GPU row order."""
+    device = _model_device(clip_model)
+    dim = clip_model.config.vision_width
+
+    def enc(x):
+        return clip_model.encode_image(x.to(device, non_blocking=True), normalize=normalize)
+    feats, labels = [], []
+    for images, target in loader:
+        feats.append(sharded_encode(enc, images, group=group, dim=dim))
+        labels.append(target.to(device))
+    return torch.cat(feats), torch.cat(labels)

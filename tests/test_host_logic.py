@@ -1,0 +1,91 @@
+"""CPU: host-side logic of the drop-in surface (no kernels run here)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import miclip
+from miclip.configs import MODEL_CONFIGS, config_from_state_dict, algorithmic_gflop_per_image
+from miclip.feature_cache import (_canonical_backbone_name, _embedding_cache_dir,
+                                  _feature_cache_dir, _feature_cache_exists, shard_range)
+from miclip.weights import param_specs
+
+REF_BPE = "/root/reference/clip/bpe_simple_vocab_16e6.txt.gz"
+
+
+@pytest.mark.parametrize("name", list(MODEL_CONFIGS))
+def test_config_inference_roundtrip(name):
+    cfg = MODEL_CONFIGS[name]
+    fake = {n: np.empty(shape, dtype=np.float32) for n, shape, _, _ in param_specs(cfg)}
+    assert config_from_state_dict(fake) == cfg
+
+
+def test_resnet_checkpoints_rejected():
+    with pytest.raises(ValueError):
+        config_from_state_dict({"visual.layer1.0.conv1.weight": np.empty((64, 64, 1, 1))})
+
+
+def test_load_errors_like_reference():
+    with pytest.raises(RuntimeError, match="not found; available models"):
+        miclip.load("RN50x64-not-a-model", device="cuda")
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="CPU-only behaviour")
+def test_product_path_has_no_cpu_fallback():
+    with pytest.raises(RuntimeError, match="HIP"):
+        miclip.load("ViT-B/32", device="cpu")
+
+
+def test_flop_model_matches_survey():
+    # 8.82 / 162.02 / 381.92 GFLOP per image
+    assert abs(algorithmic_gflop_per_image(MODEL_CONFIGS["ViT-B/32"]) - 8.82) < 0.01
+    assert abs(algorithmic_gflop_per_image(MODEL_CONFIGS["ViT-L/14"]) - 162.02) < 0.01
+    assert abs(algorithmic_gflop_per_image(MODEL_CONFIGS["ViT-L/14@336px"]) - 381.92) < 0.01
+
+
+def test_cache_paths_match_reference_layout(tmp_path):
+    cfg = {"root_path": str(tmp_path), "clip_backend": "openai", "backbone": "ViT-B/32",
+           "dataset": "cs", "shots": 0, "seed": 1, "finetune": {}}
+    assert _feature_cache_dir(cfg) == tmp_path / "features_ViTB32_cs" / "0_shot" / "seed1"
+    assert _embedding_cache_dir(cfg, "Test") == tmp_path / "feat_cache_vis" / "ViTB32_cs" / "test" / "seed1"
+    assert _canonical_backbone_name("hf-hub:timm/ViT-SO400M-14-SigLIP") == "hf-hub_timm_ViT-SO400M-14-SigLIP"
+    d = _feature_cache_dir(cfg)
+    assert not _feature_cache_exists(d, 2)
+    d.mkdir(parents=True)
+    for f in ("label.pth", "f0.pth", "f1.pth"):
+        (d / f).write_bytes(b"x")
+    assert _feature_cache_exists(d, 2) and not _feature_cache_exists(d, 3)
+
+
+@pytest.mark.parametrize("n,world", [(256, 8), (7, 2), (1, 2), (0, 4), (255, 8)])
+def test_shard_range_partitions(n, world):
+    spans = [shard_range(n, r, world) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == n
+    assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    sizes = [hi - lo for lo, hi in spans]
+    assert max(sizes) - min(sizes) <= 1
+
+
+@pytest.mark.skipif(not os.path.isfile(REF_BPE), reason="BPE vocabulary not available")
+def test_tokenizer_matches_reference_tokens(golden, monkeypatch):
+    monkeypatch.setenv("MICLIP_BPE_PATH", REF_BPE)
+    import miclip.tokenizer as tk
+    tk._tok = None
+    for tag in ("vitb32", "vitl14"):
+        g = golden(tag)
+        got = miclip.tokenize(g["meta"]["prompts"])
+        assert np.array_equal(got.numpy(), g["tokens"].astype(np.int64))
+    with pytest.raises(RuntimeError, match="too long"):
+        miclip.tokenize("word " * 100)
+    t = miclip.tokenize("word " * 100, truncate=True)
+    assert t.shape == (1, 77) and t[0, -1] == 49407
+
+
+def test_preprocess_shapes():
+    from PIL import Image
+    _, _, pre = None, None, miclip._transform(224)
+    img = Image.fromarray((np.random.default_rng(0).random((300, 400, 3)) * 255).astype(np.uint8))
+    x = pre(img)
+    assert x.shape == (3, 224, 224) and x.dtype == torch.float32
+    assert -2.5 < float(x.min()) and float(x.max()) < 2.7
