@@ -560,16 +560,17 @@ void miclip_model_destroy(miclip_model* m) {
 int64_t miclip_model_bytes(const miclip_model* m) { return m ? m->bytes : 0; }
 
 int miclip_op_gemm(int32_t dtype, const void* A, const void* W, const float* bias, void* C,
-                   int32_t M, int32_t N, int32_t K, int32_t epi, int32_t act, void* stream) {
+                   int32_t M, int32_t N, int32_t K, int32_t epi, int32_t act, int32_t variant,
+                   void* stream) {
   if (!A || !W || !C) return fail(MICLIP_EINVAL, "null argument");
   hipStream_t s = (hipStream_t)stream;
   if (epi == 0) {
-    MICLIP_HIP(gemm_store(dtype, A, W, bias, C, M, N, K, act, s));
+    MICLIP_HIP(gemm_store(dtype, A, W, bias, C, M, N, K, act, s, variant));
   } else if (epi == 1) {
     if (!bias) return fail(MICLIP_EINVAL, "residual epilogue needs a bias");
-    MICLIP_HIP(gemm_residual(dtype, A, W, bias, (float*)C, M, N, K, s));
+    MICLIP_HIP(gemm_residual(dtype, A, W, bias, (float*)C, M, N, K, s, variant));
   } else if (epi == 2) {
-    MICLIP_HIP(gemm_f32(dtype, A, W, bias, (float*)C, M, N, K, s));
+    MICLIP_HIP(gemm_f32(dtype, A, W, bias, (float*)C, M, N, K, s, variant));
   } else {
     return fail(MICLIP_EINVAL, "unknown epilogue");
   }

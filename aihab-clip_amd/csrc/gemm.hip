@@ -25,11 +25,27 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdlib>
+
 namespace miclip {
 
 namespace {
 
 constexpr int BK = 64;
+
+// Epilogue functors. The kernels hoist the per-column bias load (`bias4` /
+// `bias1`, once per column a thread owns) and then call `put4` (4 consecutive
+// columns of one row, 16-B aligned) or `put1` with the raw fp32 accumulator.
+MICLIP_DEV float4 ld_bias4(const float* b, int col) {
+  return b ? *(const float4*)(b + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+template <int ACT>
+MICLIP_DEV float act_fn(float v) {
+  if (ACT == ACT_QUICKGELU) return v / (1.0f + __expf(-1.702f * v));   // clip/model.py:160-162
+  if (ACT == ACT_GELU) return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+  return v;
+}
 
 // The activation is a template parameter so that the QKV projection (no
 // activation) and the MLP c_fc (QuickGELU) are distinct kernels in a profile.
@@ -38,14 +54,18 @@ struct EpiStore {
   T* C;
   const float* bias;
   int ldc;
-  MICLIP_DEV void operator()(int r, int c, float v) const {
-    if (bias) v += bias[c];
-    if (ACT == ACT_QUICKGELU) {
-      v = v / (1.0f + __expf(-1.702f * v));
-    } else if (ACT == ACT_GELU) {
-      v = 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
-    }
-    C[(size_t)r * ldc + c] = to_t<T>(v);
+  MICLIP_DEV float4 bias4(int col) const { return ld_bias4(bias, col); }
+  MICLIP_DEV float bias1(int col) const { return bias ? bias[col] : 0.f; }
+  MICLIP_DEV void put4(int r, int c, float4 v, float4 b) const {
+    i16x4 o;
+    o[0] = to_bits<T>(act_fn<ACT>(v.x + b.x));
+    o[1] = to_bits<T>(act_fn<ACT>(v.y + b.y));
+    o[2] = to_bits<T>(act_fn<ACT>(v.z + b.z));
+    o[3] = to_bits<T>(act_fn<ACT>(v.w + b.w));
+    *(i16x4*)(C + (size_t)r * ldc + c) = o;
+  }
+  MICLIP_DEV void put1(int r, int c, float v, float b) const {
+    C[(size_t)r * ldc + c] = to_t<T>(act_fn<ACT>(v + b));
   }
 };
 
@@ -53,9 +73,16 @@ struct EpiResidual {
   float* X;
   const float* bias;
   int ldx;
-  MICLIP_DEV void operator()(int r, int c, float v) const {
+  MICLIP_DEV float4 bias4(int col) const { return ld_bias4(bias, col); }
+  MICLIP_DEV float bias1(int col) const { return bias[col]; }
+  MICLIP_DEV void put4(int r, int c, float4 v, float4 b) const {
+    float4* p = (float4*)(X + (size_t)r * ldx + c);
+    const float4 x = *p;
+    *p = make_float4(x.x + (v.x + b.x), x.y + (v.y + b.y), x.z + (v.z + b.z), x.w + (v.w + b.w));
+  }
+  MICLIP_DEV void put1(int r, int c, float v, float b) const {
     float* p = X + (size_t)r * ldx + c;
-    *p = *p + (v + bias[c]);
+    *p = *p + (v + b);
   }
 };
 
@@ -63,9 +90,12 @@ struct EpiF32 {
   float* C;
   const float* bias;
   int ldc;
-  MICLIP_DEV void operator()(int r, int c, float v) const {
-    C[(size_t)r * ldc + c] = bias ? v + bias[c] : v;
+  MICLIP_DEV float4 bias4(int col) const { return ld_bias4(bias, col); }
+  MICLIP_DEV float bias1(int col) const { return bias ? bias[col] : 0.f; }
+  MICLIP_DEV void put4(int r, int c, float4 v, float4 b) const {
+    *(float4*)(C + (size_t)r * ldc + c) = make_float4(v.x + b.x, v.y + b.y, v.z + b.z, v.w + b.w);
   }
+  MICLIP_DEV void put1(int r, int c, float v, float b) const { C[(size_t)r * ldc + c] = v + b; }
 };
 
 struct EpiPatch {
@@ -73,10 +103,19 @@ struct EpiPatch {
   const float* pos;
   int ldx;
   int np;
-  MICLIP_DEV void operator()(int r, int c, float v) const {
-    const int b = r / np, p = r - b * np;
-    const size_t row = (size_t)b * (np + 1) + 1 + p;
-    X[row * ldx + c] = v + pos[(size_t)(1 + p) * ldx + c];
+  MICLIP_DEV float4 bias4(int) const { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  MICLIP_DEV float bias1(int) const { return 0.f; }
+  MICLIP_DEV size_t row_of(int r) const {
+    const int b = r / np;
+    return (size_t)b * (np + 1) + 1 + (r - b * np);
+  }
+  MICLIP_DEV void put4(int r, int c, float4 v, float4) const {
+    const int p = r % np;
+    const float4 q = *(const float4*)(pos + (size_t)(1 + p) * ldx + c);
+    *(float4*)(X + row_of(r) * ldx + c) = make_float4(v.x + q.x, v.y + q.y, v.z + q.z, v.w + q.w);
+  }
+  MICLIP_DEV void put1(int r, int c, float v, float) const {
+    X[row_of(r) * ldx + c] = v + pos[(size_t)(1 + r % np) * ldx + c];
   }
 };
 
@@ -172,17 +211,199 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const T* __restrict__ A,
   }
 
 #pragma unroll
-  for (int i = 0; i < FM; ++i) {
+  for (int j = 0; j < FN; ++j) {
+    const int col = n0 + wn * TN + j * 16 + fr;
+    const float b = epi.bias1(col);
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int col = n0 + wn * TN + j * 16 + fr;
+    for (int i = 0; i < FM; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wm * TM + i * 16 + fk * 4 + r;
-        if (row < M) epi(row, col, acc[i][j][r]);
+        if (row < M) epi.put1(row, col, acc[i][j][r], b);
       }
     }
   }
+}
+
+
+// ---------------------------------------------------------------------------
+// 256x256x64 tile, 512 threads = 8 waves as 2(M) x 4(N), 128x64 per wave.
+// LDS: 2 buffers x 4 half-tile slots {A0, A1, B0, B1} x 16 KiB = 128 KiB
+// (1 workgroup per CU). Slot A_h holds tile rows {wr*128 + h*64 + 0..63},
+// slot B_h tile cols {wc*64 + h*32 + 0..31}, so wave quadrant (qi, qj) reads
+// exactly slots A_qi and B_qj. Each K-tile runs as 4 phases (quadrants
+// Q0=(0,0) Q1=(0,1) Q2=(1,1) Q3=(1,0), 16 MFMAs each); every phase issues one
+// half-tile of LDS-DMA (2 x global_load_lds_dwordx4 per lane) into a slot
+// whose last reader finished before that phase's barrier:
+//   phase 0: A1(t+1)   phase 1: B0(t+1)   phase 2: A0(t+2)   phase 3: B1(t+2)
+// so one K-tile's data is in flight across the K-tile boundary and the only
+// wait is a counted `s_waitcnt vmcnt(4)` once per K-tile (never 0 in the
+// main loop; cdna_hip_programming.md §5 "Pipelining across barriers", T3/T4).
+// ---------------------------------------------------------------------------
+MICLIP_DEV void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <typename T, class Epi>
+__global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
+                                                      const T* __restrict__ W, int M, int N,
+                                                      int K, Epi epi) {
+  constexpr int HALF = 128 * 128;  // bytes of one half-tile slot
+  constexpr int EPI_LD = 260;      // fp32 row stride of the epilogue staging (pad 4)
+  constexpr int SMEM = 128 * EPI_LD * 4 > 8 * HALF ? 128 * EPI_LD * 4 : 8 * HALF;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int ntn = N / 256, ntm = (M + 255) / 256;
+  const int bid = xcd_remap(blockIdx.x, ntm * ntn);
+  const int tm = bid / ntn, tn = bid - tm * ntn;
+  const int m0 = tm * 256, n0 = tn * 256;
+
+  // LDS-DMA sources: slot row sr = piece*8 + (lane>>3), piece = wave*2 + pp
+  const int lchunk = (lane & 7) ^ (lane >> 3);
+  const T* asrc[2][2];
+  const T* bsrc[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      const int sr = (wave * 2 + pp) * 8 + (lane >> 3);
+      int ar = m0 + (sr >> 6) * 128 + h * 64 + (sr & 63);
+      ar = ar < M ? ar : M - 1;
+      asrc[h][pp] = A + (size_t)ar * K + lchunk * 8;
+      const int bc = n0 + (sr >> 5) * 64 + h * 32 + (sr & 31);
+      bsrc[h][pp] = W + (size_t)bc * K + lchunk * 8;
+    }
+  // slot index: buf*4 + {0:A0, 1:A1, 2:B0, 3:B1}
+  auto stage = [&](int slot_kind, int tile) {
+    const int buf = tile & 1, k0 = tile * 64;
+    char* dst = smem + (buf * 4 + slot_kind) * HALF + wave * 2048;
+    const T* const* src = slot_kind < 2 ? asrc[slot_kind] : bsrc[slot_kind - 2];
+    glds16(src[0] + k0, dst);
+    glds16(src[1] + k0, dst + 1024);
+  };
+
+  const int fr = lane & 15, fk = lane >> 4;
+  // byte offsets inside a slot for k-step s (swizzled 16-B chunk), per fragment row
+  const int aoff = (wr * 64 + fr) * 128, boff = (wc * 32 + fr) * 128;
+  const int sw0 = ((0 + fk) ^ (fr & 7)) << 4, sw1 = ((4 + fk) ^ (fr & 7)) << 4;
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / 64;
+  // prologue: A0(0) B1(0) A1(0) B0(0) A0(1) B1(1)
+  stage(0, 0);
+  stage(3, 0);
+  stage(1, 0);
+  stage(2, 0);
+  if (nk > 1) {
+    stage(0, 1);
+    stage(3, 1);
+  }
+
+  i16x8 af[2][4], bf[2][2];
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    const char* sA0 = smem + (buf * 4 + 0) * HALF + aoff;
+    const char* sA1 = smem + (buf * 4 + 1) * HALF + aoff;
+    const char* sB0 = smem + (buf * 4 + 2) * HALF + boff;
+    const char* sB1 = smem + (buf * 4 + 3) * HALF + boff;
+    if (t + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      lds_barrier();
+      const int qi = (p >= 2) ? 1 : 0;
+      const int qj = (p == 1 || p == 2) ? 1 : 0;
+      if (p == 0 || p == 2) {
+        const char* sa = qi ? sA1 : sA0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          af[0][i] = *(const i16x8*)(sa + i * 2048 + sw0);
+          af[1][i] = *(const i16x8*)(sa + i * 2048 + sw1);
+        }
+      }
+      {
+        const char* sb = qj ? sB1 : sB0;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          bf[0][j] = *(const i16x8*)(sb + j * 2048 + sw0);
+          bf[1][j] = *(const i16x8*)(sb + j * 2048 + sw1);
+        }
+      }
+      if (p == 0 && t + 1 < nk) stage(1, t + 1);
+      if (p == 1 && t + 1 < nk) stage(2, t + 1);
+      if (p == 2 && t + 2 < nk) stage(0, t + 2);
+      if (p == 3 && t + 2 < nk) stage(3, t + 2);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[qi][qj][i][j] = Mfma<T>::m16(af[s][i], bf[s][j], acc[qi][qj][i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+
+  // Epilogue through LDS: two passes (quadrant row qi), each stages the WG's
+  // 128 x 256 fp32 accumulator rows {wr*128 + qi*64 + 0..63} in LDS (row stride
+  // 260 floats: the 4 fk row groups of a ds_write_b32 land on distinct banks),
+  // then every wave streams whole 1-KiB rows out: 16-B loads/stores per lane,
+  // bias hoisted per column, residual/activation applied on the way out.
+  float* stg = (float*)smem;
+  const int ec = (tid & 63) * 4;            // this thread's 4 output columns
+  const float4 bv = epi.bias4(n0 + ec);
+  const bool full = m0 + 256 <= M;
+#pragma unroll
+  for (int qi = 0; qi < 2; ++qi) {
+    lds_barrier();
+#pragma unroll
+    for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int lr = wr * 64 + i * 16 + fk * 4 + r;      // staged row 0..127
+            const int lc = wc * 64 + qj * 32 + j * 16 + fr;    // col 0..255
+            stg[lr * EPI_LD + lc] = acc[qi][qj][i][j][r];
+          }
+    lds_barrier();
+#pragma unroll 4
+    for (int k = 0; k < 16; ++k) {
+      const int lr = (tid >> 6) + 8 * k;                      // 0..127
+      const int row = m0 + (lr >> 6) * 128 + qi * 64 + (lr & 63);
+      const float4 v = *(const float4*)(stg + lr * EPI_LD + ec);
+      if (full || row < M) epi.put4(row, n0 + ec, v, bv);
+    }
+  }
+}
+
+// MICLIP_GEMM=128 forces the 128x128 kernel (A/B comparisons), 256 forces the
+// 256x256 one wherever the shape allows; default picks by problem size.
+int gemm_variant() {
+  static int v = [] {
+    const char* e = getenv("MICLIP_GEMM");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 bool gemm_shape_ok(int M, int N, int K) {
@@ -190,8 +411,19 @@ bool gemm_shape_ok(int M, int N, int K) {
 }
 
 template <typename T, class Epi>
-hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hipStream_t s) {
+hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hipStream_t s,
+                  int variant = 0) {
   if (!gemm_shape_ok(M, N, K)) return hipErrorInvalidValue;
+  if (variant == 0) variant = gemm_variant();
+  if (variant != 0 && variant != 128 && variant != 256) return hipErrorInvalidValue;
+  // Large problems: 256x256 tile (1 WG/CU, L2-friendly arithmetic intensity);
+  // small ones (text tower, tiny batches) keep more workgroups with 128x128.
+  const int tiles256 = ((M + 255) / 256) * (N / 256);
+  if (N % 256 == 0 && variant != 128 && (tiles256 >= 256 || variant == 256)) {
+    hipLaunchKernelGGL((gemm256_kernel<T, Epi>), dim3(tiles256), dim3(512), 0, s, (const T*)A,
+                       (const T*)W, M, N, K, epi);
+    return hipGetLastError();
+  }
   constexpr int BM = 128, BN = 128;
   const int grid = ((M + BM - 1) / BM) * (N / BN);
   hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, Epi>), dim3(grid), dim3(256), 0, s,
@@ -203,35 +435,35 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
 
 template <typename T>
 hipError_t gemm_store_t(const void* A, const void* W, const float* bias, void* C, int M, int N,
-                        int K, int act, hipStream_t s) {
+                        int K, int act, hipStream_t s, int v) {
   switch (act) {
     case ACT_NONE:
-      return launch<T>(A, W, M, N, K, EpiStore<T, ACT_NONE>{(T*)C, bias, N}, s);
+      return launch<T>(A, W, M, N, K, EpiStore<T, ACT_NONE>{(T*)C, bias, N}, s, v);
     case ACT_QUICKGELU:
-      return launch<T>(A, W, M, N, K, EpiStore<T, ACT_QUICKGELU>{(T*)C, bias, N}, s);
+      return launch<T>(A, W, M, N, K, EpiStore<T, ACT_QUICKGELU>{(T*)C, bias, N}, s, v);
     case ACT_GELU:
-      return launch<T>(A, W, M, N, K, EpiStore<T, ACT_GELU>{(T*)C, bias, N}, s);
+      return launch<T>(A, W, M, N, K, EpiStore<T, ACT_GELU>{(T*)C, bias, N}, s, v);
     default:
       return hipErrorInvalidValue;
   }
 }
 
 hipError_t gemm_store(int dtype, const void* A, const void* W, const float* bias, void* C, int M,
-                      int N, int K, int act, hipStream_t s) {
-  if (dtype == kF16) return gemm_store_t<_Float16>(A, W, bias, C, M, N, K, act, s);
-  return gemm_store_t<__bf16>(A, W, bias, C, M, N, K, act, s);
+                      int N, int K, int act, hipStream_t s, int v) {
+  if (dtype == kF16) return gemm_store_t<_Float16>(A, W, bias, C, M, N, K, act, s, v);
+  return gemm_store_t<__bf16>(A, W, bias, C, M, N, K, act, s, v);
 }
 
 hipError_t gemm_residual(int dtype, const void* A, const void* W, const float* bias, float* X,
-                         int M, int N, int K, hipStream_t s) {
-  if (dtype == kF16) return launch<_Float16>(A, W, M, N, K, EpiResidual{X, bias, N}, s);
-  return launch<__bf16>(A, W, M, N, K, EpiResidual{X, bias, N}, s);
+                         int M, int N, int K, hipStream_t s, int v) {
+  if (dtype == kF16) return launch<_Float16>(A, W, M, N, K, EpiResidual{X, bias, N}, s, v);
+  return launch<__bf16>(A, W, M, N, K, EpiResidual{X, bias, N}, s, v);
 }
 
 hipError_t gemm_f32(int dtype, const void* A, const void* W, const float* bias, float* C, int M,
-                    int N, int K, hipStream_t s) {
-  if (dtype == kF16) return launch<_Float16>(A, W, M, N, K, EpiF32{C, bias, N}, s);
-  return launch<__bf16>(A, W, M, N, K, EpiF32{C, bias, N}, s);
+                    int N, int K, hipStream_t s, int v) {
+  if (dtype == kF16) return launch<_Float16>(A, W, M, N, K, EpiF32{C, bias, N}, s, v);
+  return launch<__bf16>(A, W, M, N, K, EpiF32{C, bias, N}, s, v);
 }
 
 hipError_t gemm_patch(int dtype, const void* A, const void* W, const float* pos, float* X, int M,

@@ -12,14 +12,15 @@ enum Act { ACT_NONE = 0, ACT_QUICKGELU = 1, ACT_GELU = 2 };
 // ---- GEMM: C[M,N] = A[M,K] . W[N,K]^T (+ epilogue); A, W in compute dtype ----
 // Shapes: N % 128 == 0, K % 64 == 0, any M >= 1; A, W rows K-contiguous.
 // Store epilogue: C (compute dtype, ld = N) = act(acc + bias).
+// `variant`: 0 = pick by size, 128 / 256 = force that tile (tests, A/B timing).
 hipError_t gemm_store(int dtype, const void* A, const void* W, const float* bias, void* C,
-                      int M, int N, int K, int act, hipStream_t s);
+                      int M, int N, int K, int act, hipStream_t s, int variant = 0);
 // Residual epilogue: X (fp32, ld = N) += acc + bias.
 hipError_t gemm_residual(int dtype, const void* A, const void* W, const float* bias, float* X,
-                         int M, int N, int K, hipStream_t s);
+                         int M, int N, int K, hipStream_t s, int variant = 0);
 // Float epilogue: C (fp32, ld = N) = acc + bias (bias may be null).
 hipError_t gemm_f32(int dtype, const void* A, const void* W, const float* bias, float* C,
-                    int M, int N, int K, hipStream_t s);
+                    int M, int N, int K, hipStream_t s, int variant = 0);
 // Patch-embed epilogue: row m = b*np + p of the patch GEMM goes to token row
 // b*(np+1) + 1 + p of X (fp32, ld = N), plus positional embedding row 1 + p.
 hipError_t gemm_patch(int dtype, const void* A, const void* W, const float* pos, float* X,

@@ -74,7 +74,7 @@ def load_library(path: str = None):
         "miclip_model_bytes": ([vp], i64),
         "miclip_set_profiling": ([vp, ctypes.c_int], ctypes.c_int),
         "miclip_profile_read": ([vp, ctypes.POINTER(MiclipKernelStat), i32, i32], ctypes.c_int),
-        "miclip_op_gemm": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp], ctypes.c_int),
+        "miclip_op_gemm": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp], ctypes.c_int),
         "miclip_op_layernorm": ([i32, vp, vp, vp, vp, i32, i32, i32, vp], ctypes.c_int),
         "miclip_op_attention": ([i32, vp, vp, i32, i32, i32, i32, vp], ctypes.c_int),
     }

@@ -1,0 +1,101 @@
+#!/usr/bin/env python
+"""Per-op micro-benchmark of the HIP kernels at the ViT-L/14 bs=256 shapes.
+
+Times each op with HIP events on torch's current stream over `--iters`
+launches (random operands: zero data inflates MFMA clocks) and prints one
+JSON line per op with algorithmic TFLOP/s and GB/s.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "aihab-clip_amd"))
+
+import torch  # noqa: E402
+
+from miclip import _lib  # noqa: E402
+
+
+def timeit(fn, iters, warm=3):
+    for _ in range(warm):
+        fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--width", type=int, default=1024)
+    ap.add_argument("--tokens", type=int, default=257)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--variants", default="128,256")
+    ap.add_argument("--ops", default="gemm,attention,layernorm")
+    args = ap.parse_args()
+    lib = _lib.load_library()
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    M, W = args.batch * args.tokens, args.width
+    dt = torch.float16
+    g = torch.Generator(device="cuda").manual_seed(0)
+    out = []
+    if "gemm" in args.ops:
+        A = (torch.randn(M, 4 * W, device="cuda", generator=g) * 0.5).to(dt)
+        Wt = (torch.randn(4 * W, 4 * W, device="cuda", generator=g) * 0.02).to(dt)
+        bias = torch.randn(4 * W, device="cuda", generator=g) * 0.02
+        C16 = torch.empty(M, 4 * W, device="cuda", dtype=dt)
+        X = torch.randn(M, W, device="cuda", generator=g)
+        shapes = [("qkv", 3 * W, W, 0, 0), ("out", W, W, 1, 0), ("fc", 4 * W, W, 0, 1),
+                  ("proj", W, 4 * W, 1, 0)]
+        for v in [int(x) for x in args.variants.split(",")]:
+            for name, N, K, epi, act in shapes:
+                C = X if epi == 1 else C16
+
+                def fn():
+                    rc = lib.miclip_op_gemm(0, A.data_ptr(), Wt.data_ptr(), bias.data_ptr(), C.data_ptr(),
+                                            M, N, K, epi, act, v, s)
+                    assert rc == 0, lib.miclip_last_error()
+                ms = timeit(fn, args.iters)
+                fl = 2.0 * M * N * K
+                by = 2.0 * M * K + 2.0 * N * K + (8.0 if epi == 1 else 2.0) * M * N
+                out.append(dict(op=f"gemm_{name}", variant=v, M=M, N=N, K=K, ms=round(ms, 4),
+                                tflops=round(fl / ms / 1e9, 1), gbs=round(by / ms / 1e6, 1)))
+                print(json.dumps(out[-1]), flush=True)
+        del A, Wt, C16, X
+    if "attention" in args.ops:
+        H = W // 64
+        qkv = (torch.randn(M, 3 * W, device="cuda", generator=g)).to(dt)
+        o = torch.empty(M, W, device="cuda", dtype=dt)
+
+        def fa():
+            rc = lib.miclip_op_attention(0, qkv.data_ptr(), o.data_ptr(), args.batch, args.tokens, H, 0, s)
+            assert rc == 0
+        ms = timeit(fa, args.iters)
+        fl = 4.0 * args.batch * H * args.tokens ** 2 * 64
+        out.append(dict(op="attention", B=args.batch, N=args.tokens, H=H, ms=round(ms, 4),
+                        tflops=round(fl / ms / 1e9, 1), gbs=round(4.0 * M * W * 2 / ms / 1e6, 1)))
+        print(json.dumps(out[-1]), flush=True)
+    if "layernorm" in args.ops:
+        x = torch.randn(M, W, device="cuda", generator=g)
+        gm = torch.ones(W, device="cuda")
+        bt = torch.zeros(W, device="cuda")
+        y = torch.empty(M, W, device="cuda", dtype=dt)
+
+        def fl_():
+            assert lib.miclip_op_layernorm(0, x.data_ptr(), gm.data_ptr(), bt.data_ptr(), y.data_ptr(),
+                                           0, M, W, s) == 0
+        ms = timeit(fl_, args.iters)
+        out.append(dict(op="layernorm", M=M, D=W, ms=round(ms, 4), gbs=round(M * W * 6 / ms / 1e6, 1)))
+        print(json.dumps(out[-1]), flush=True)
+
+
+if __name__ == "__main__":
+    main()

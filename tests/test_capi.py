@@ -62,6 +62,6 @@ def test_abi_version_and_validation(lib):
     assert rc == -1
     assert b"vision_width" in lib.miclip_last_error()
     assert lib.miclip_model_create(None, 0, ctypes.byref(h)) == -1
-    assert lib.miclip_op_gemm(0, None, None, None, None, 1, 128, 64, 0, 0, None) == -1
+    assert lib.miclip_op_gemm(0, None, None, None, None, 1, 128, 64, 0, 0, 0, None) == -1
     lib.miclip_model_destroy(None)           # no-op on NULL
     assert lib.miclip_model_bytes(None) == 0

@@ -30,9 +30,12 @@ def _check(lib, rc):
 
 
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
-@pytest.mark.parametrize("M,N,K", [(300, 256, 192), (128, 128, 64), (65, 384, 1024), (1000, 768, 3072)])
+@pytest.mark.parametrize("M,N,K,variant", [(300, 256, 192, 0), (128, 128, 64, 0), (65, 384, 1024, 0),
+                                          (1000, 768, 3072, 128), (1000, 768, 3072, 256),
+                                          (300, 256, 192, 256), (257, 512, 64, 256),
+                                          (4096, 1024, 1024, 0), (33, 2304, 768, 256)])
 @pytest.mark.parametrize("epi,act", [(0, 0), (0, 1), (0, 2), (1, 0), (2, 0)])
-def test_gemm(lib, dt, M, N, K, epi, act):
+def test_gemm(lib, dt, M, N, K, variant, epi, act):
     code, tdt = DT[dt]
     g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K + epi * 3 + act)
     A = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(tdt)
@@ -52,7 +55,7 @@ def test_gemm(lib, dt, M, N, K, epi, act):
     else:
         C = torch.empty(M, N, device="cuda", dtype=torch.float32)
     _check(lib, lib.miclip_op_gemm(code, A.data_ptr(), W.data_ptr(), bias.data_ptr(), C.data_ptr(),
-                                   M, N, K, epi, act, _stream()))
+                                   M, N, K, epi, act, variant, _stream()))
     torch.cuda.synchronize()
     err = (C.float() - ref).abs().max().item()
     tol = (2e-2 if dt == "bf16" else 4e-3) * max(1.0, ref.abs().max().item()) if epi == 0 else 2e-4 * K ** 0.5
@@ -63,8 +66,13 @@ def test_gemm_rejects_bad_shapes(lib):
     A = torch.zeros(16, 64, device="cuda", dtype=torch.float16)
     W = torch.zeros(100, 64, device="cuda", dtype=torch.float16)
     C = torch.zeros(16, 100, device="cuda", dtype=torch.float16)
-    rc = lib.miclip_op_gemm(0, A.data_ptr(), W.data_ptr(), None, C.data_ptr(), 16, 100, 64, 0, 0, _stream())
+    rc = lib.miclip_op_gemm(0, A.data_ptr(), W.data_ptr(), None, C.data_ptr(), 16, 100, 64, 0, 0, 0, _stream())
     assert rc == -1
+    # 256 tile needs N % 256 == 0
+    W2 = torch.zeros(384, 64, device="cuda", dtype=torch.float16)
+    C2 = torch.zeros(16, 384, device="cuda", dtype=torch.float16)
+    assert lib.miclip_op_gemm(0, A.data_ptr(), W2.data_ptr(), None, C2.data_ptr(), 16, 384, 64, 0, 0, 256, _stream()) == 0
+    torch.cuda.synchronize()
 
 
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
