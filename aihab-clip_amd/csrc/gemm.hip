@@ -42,7 +42,8 @@ MICLIP_DEV float4 ld_bias4(const float* b, int col) {
 
 template <int ACT>
 MICLIP_DEV float act_fn(float v) {
-  if (ACT == ACT_QUICKGELU) return v / (1.0f + __expf(-1.702f * v));   // clip/model.py:160-162
+  // x * sigmoid(1.702 x) (clip/model.py:160-162): v_exp + v_rcp, no IEEE divide
+  if (ACT == ACT_QUICKGELU) return v * __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v));
   if (ACT == ACT_GELU) return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
   return v;
 }
