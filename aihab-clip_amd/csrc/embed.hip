@@ -94,54 +94,80 @@ __global__ __launch_bounds__(256) void rowvec_matmul_kernel(const float* __restr
   out[(size_t)r * E + e] = acc;
 }
 
+// ROWS images per workgroup: every visual.proj element read from L2 feeds ROWS
+// FMAs (the projection is the only real work: 2*Din*E flops per image).
+template <int ROWS>
 __global__ __launch_bounds__(256) void zero_shot_kernel(const float* __restrict__ x,
                                                         const float* __restrict__ proj,
                                                         const float* __restrict__ tw,
                                                         float* __restrict__ logits,
-                                                        int32_t* __restrict__ topk, int Din,
-                                                        int E, int C, float scale, int k) {
+                                                        int32_t* __restrict__ topk, int B,
+                                                        int Din, int E, int C, float scale,
+                                                        int k) {
   extern __shared__ float sm[];
-  float* xs = sm;          // Din
-  float* fs = xs + Din;    // E
-  float* ls = fs + E;      // C
-  float* red = ls + C;     // 4
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int d = tid; d < Din; d += 256) xs[d] = x[(size_t)b * Din + d];
+  float* xs = sm;                 // [ROWS][Din]
+  float* fs = xs + ROWS * Din;    // [ROWS][E]
+  float* ls = fs + ROWS * E;      // [ROWS][C]
+  float* red = ls + ROWS * C;     // [ROWS][4] partial norms, then [ROWS] inverse norms
+  const int b0 = blockIdx.x * ROWS, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nr = B - b0 < ROWS ? B - b0 : ROWS;
+  for (int i = tid; i < ROWS * Din; i += 256) {
+    const int r = i / Din;
+    xs[i] = r < nr ? x[(size_t)(b0 + r) * Din + (i - r * Din)] : 0.f;
+  }
   __syncthreads();
-  float n2 = 0.f;
+  float n2[ROWS];
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r) n2[r] = 0.f;
   for (int e = tid; e < E; e += 256) {
-    float acc;
+    float acc[ROWS];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) acc[r] = proj ? 0.f : xs[r * Din + e];
     if (proj) {
-      acc = 0.f;
-      for (int d = 0; d < Din; ++d) acc = fmaf(xs[d], proj[(size_t)d * E + e], acc);
-    } else {
-      acc = xs[e];
+      for (int d = 0; d < Din; ++d) {
+        const float wv = proj[(size_t)d * E + e];
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) acc[r] = fmaf(xs[r * Din + d], wv, acc[r]);
+      }
     }
-    fs[e] = acc;
-    n2 += acc * acc;
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) {
+      fs[r * E + e] = acc[r];
+      n2[r] += acc[r] * acc[r];
+    }
   }
-  n2 = wave_sum(n2);
-  if (lane == 0) red[w] = n2;
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r) {
+    const float v = wave_sum(n2[r]);
+    if (lane == 0) red[r * 4 + w] = v;
+  }
   __syncthreads();
-  const float inv = 1.0f / fmaxf(sqrtf(red[0] + red[1] + red[2] + red[3]), 1e-12f);
-  for (int c = tid; c < C; c += 256) {
+  if (tid < ROWS) {
+    const float t = red[tid * 4] + red[tid * 4 + 1] + red[tid * 4 + 2] + red[tid * 4 + 3];
+    red[ROWS * 4 + tid] = 1.0f / fmaxf(sqrtf(t), 1e-12f);   // F.normalize eps
+  }
+  __syncthreads();
+  for (int i = tid; i < nr * C; i += 256) {
+    const int r = i / C, c = i - r * C;
+    const float inv = red[ROWS * 4 + r];
     float acc = 0.f;
-    for (int e = 0; e < E; ++e) acc = fmaf(fs[e] * inv, tw[(size_t)e * C + c], acc);
-    ls[c] = scale * acc;
-    logits[(size_t)b * C + c] = scale * acc;
+    for (int e = 0; e < E; ++e) acc = fmaf(fs[r * E + e] * inv, tw[(size_t)e * C + c], acc);
+    ls[r * C + c] = scale * acc;
+    logits[(size_t)(b0 + r) * C + c] = scale * acc;
   }
   __syncthreads();
-  if (tid == 0 && topk) {
+  if (topk && tid < nr) {
     // selection of the k largest, ties -> lower index first (sorted, largest first)
+    float* l = ls + tid * C;
     for (int j = 0; j < k; ++j) {
       int bi = -1;
       float bv = -INFINITY;
       for (int c = 0; c < C; ++c) {
-        const float v = ls[c];
+        const float v = l[c];
         if (bi < 0 || v > bv) { bv = v; bi = c; }
       }
-      topk[(size_t)b * k + j] = bi;
-      ls[bi] = -INFINITY;
+      topk[(size_t)(b0 + tid) * k + j] = bi;
+      l[bi] = -INFINITY;
     }
   }
 }
@@ -202,10 +228,16 @@ hipError_t zero_shot(const float* x, const float* proj, const float* tw, float* 
                      int32_t* topk, int B, int Din, int E, int C, float scale, int k,
                      hipStream_t s) {
   if (B < 1 || C < 1 || E < 1 || k < 0 || k > C || (!proj && Din != E)) return hipErrorInvalidValue;
-  const size_t sm = (size_t)(Din + E + C + 4) * sizeof(float);
-  if (sm > 64 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(zero_shot_kernel, dim3(B), dim3(256), sm, s, x, proj, tw, logits, topk, Din,
-                     E, C, scale, k);
+  const size_t per_row = (size_t)(Din + E + C + 5) * sizeof(float);
+  if (8 * per_row <= 64 * 1024) {
+    hipLaunchKernelGGL(zero_shot_kernel<8>, dim3((B + 7) / 8), dim3(256), 8 * per_row, s, x, proj,
+                       tw, logits, topk, B, Din, E, C, scale, k);
+  } else if (per_row <= 64 * 1024) {
+    hipLaunchKernelGGL(zero_shot_kernel<1>, dim3(B), dim3(256), per_row, s, x, proj, tw, logits,
+                       topk, B, Din, E, C, scale, k);
+  } else {
+    return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

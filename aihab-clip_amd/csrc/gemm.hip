@@ -247,7 +247,11 @@ MICLIP_DEV void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <typename T, class Epi>
+// SCHED 0: the half-tile schedule above (4 barriers per K-tile, ~1.5 K-tiles
+// in flight). SCHED 1: one barrier per K-tile; right after it the whole next
+// K-tile is issued (8 LDS-DMA per lane) and the 4 quadrant phases run without
+// barriers, so the compiler can pipeline fragment reads under the MFMAs.
+template <typename T, class Epi, int SCHED>
 __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
                                                       const T* __restrict__ W, int M, int N,
                                                       int K, Epi epi) {
@@ -304,61 +308,93 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
         for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / 64;
-  // prologue: A0(0) B1(0) A1(0) B0(0) A0(1) B1(1)
-  stage(0, 0);
-  stage(3, 0);
-  stage(1, 0);
-  stage(2, 0);
-  if (nk > 1) {
-    stage(0, 1);
-    stage(3, 1);
-  }
-
   i16x8 af[2][4], bf[2][2];
-  for (int t = 0; t < nk; ++t) {
-    const int buf = t & 1;
-    const char* sA0 = smem + (buf * 4 + 0) * HALF + aoff;
-    const char* sA1 = smem + (buf * 4 + 1) * HALF + aoff;
-    const char* sB0 = smem + (buf * 4 + 2) * HALF + boff;
-    const char* sB1 = smem + (buf * 4 + 3) * HALF + boff;
-    if (t + 1 < nk)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else
+  auto quadrant = [&](const char* sa, const char* sb, int qi, int qj, bool load_a) {
+    if (load_a) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        af[0][i] = *(const i16x8*)(sa + i * 2048 + sw0);
+        af[1][i] = *(const i16x8*)(sa + i * 2048 + sw1);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bf[0][j] = *(const i16x8*)(sb + j * 2048 + sw0);
+      bf[1][j] = *(const i16x8*)(sb + j * 2048 + sw1);
+    }
+  };
+  auto mfma_q = [&](int qi, int qj) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[qi][qj][i][j] = Mfma<T>::m16(af[s][i], bf[s][j], acc[qi][qj][i][j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  if constexpr (SCHED == 0) {
+    // prologue: A0(0) B1(0) A1(0) B0(0) A0(1) B1(1)
+    stage(0, 0);
+    stage(3, 0);
+    stage(1, 0);
+    stage(2, 0);
+    if (nk > 1) {
+      stage(0, 1);
+      stage(3, 1);
+    }
+    for (int t = 0; t < nk; ++t) {
+      const int buf = t & 1;
+      const char* sA0 = smem + (buf * 4 + 0) * HALF + aoff;
+      const char* sA1 = smem + (buf * 4 + 1) * HALF + aoff;
+      const char* sB0 = smem + (buf * 4 + 2) * HALF + boff;
+      const char* sB1 = smem + (buf * 4 + 3) * HALF + boff;
+      if (t + 1 < nk)
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        lds_barrier();
+        const int qi = (p >= 2) ? 1 : 0;
+        const int qj = (p == 1 || p == 2) ? 1 : 0;
+        quadrant(qi ? sA1 : sA0, qj ? sB1 : sB0, qi, qj, p == 0 || p == 2);
+        if (p == 0 && t + 1 < nk) stage(1, t + 1);
+        if (p == 1 && t + 1 < nk) stage(2, t + 1);
+        if (p == 2 && t + 2 < nk) stage(0, t + 2);
+        if (p == 3 && t + 2 < nk) stage(3, t + 2);
+        mfma_q(qi, qj);
+      }
+    }
+  } else {
+    stage(0, 0);
+    stage(2, 0);
+    stage(3, 0);
+    stage(1, 0);
+    for (int t = 0; t < nk; ++t) {
+      const int buf = t & 1;
+      const char* sA0 = smem + (buf * 4 + 0) * HALF + aoff;
+      const char* sA1 = smem + (buf * 4 + 1) * HALF + aoff;
+      const char* sB0 = smem + (buf * 4 + 2) * HALF + boff;
+      const char* sB1 = smem + (buf * 4 + 3) * HALF + boff;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
       lds_barrier();
-      const int qi = (p >= 2) ? 1 : 0;
-      const int qj = (p == 1 || p == 2) ? 1 : 0;
-      if (p == 0 || p == 2) {
-        const char* sa = qi ? sA1 : sA0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          af[0][i] = *(const i16x8*)(sa + i * 2048 + sw0);
-          af[1][i] = *(const i16x8*)(sa + i * 2048 + sw1);
-        }
+      if (t + 1 < nk) {
+        stage(0, t + 1);
+        stage(2, t + 1);
+        stage(3, t + 1);
+        stage(1, t + 1);
       }
-      {
-        const char* sb = qj ? sB1 : sB0;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          bf[0][j] = *(const i16x8*)(sb + j * 2048 + sw0);
-          bf[1][j] = *(const i16x8*)(sb + j * 2048 + sw1);
-        }
-      }
-      if (p == 0 && t + 1 < nk) stage(1, t + 1);
-      if (p == 1 && t + 1 < nk) stage(2, t + 1);
-      if (p == 2 && t + 2 < nk) stage(0, t + 2);
-      if (p == 3 && t + 2 < nk) stage(3, t + 2);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[qi][qj][i][j] = Mfma<T>::m16(af[s][i], bf[s][j], acc[qi][qj][i][j]);
-      __builtin_amdgcn_s_setprio(0);
+      quadrant(sA0, sB0, 0, 0, true);
+      mfma_q(0, 0);
+      quadrant(sA0, sB1, 0, 1, false);
+      mfma_q(0, 1);
+      quadrant(sA1, sB1, 1, 1, true);
+      mfma_q(1, 1);
+      quadrant(sA1, sB0, 1, 0, false);
+      mfma_q(1, 0);
     }
   }
 
@@ -416,13 +452,18 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
                   int variant = 0) {
   if (!gemm_shape_ok(M, N, K)) return hipErrorInvalidValue;
   if (variant == 0) variant = gemm_variant();
-  if (variant != 0 && variant != 128 && variant != 256) return hipErrorInvalidValue;
+  if (variant != 0 && variant != 128 && variant != 256 && variant != 257)
+    return hipErrorInvalidValue;
   // Large problems: 256x256 tile (1 WG/CU, L2-friendly arithmetic intensity);
   // small ones (text tower, tiny batches) keep more workgroups with 128x128.
   const int tiles256 = ((M + 255) / 256) * (N / 256);
-  if (N % 256 == 0 && variant != 128 && (tiles256 >= 256 || variant == 256)) {
-    hipLaunchKernelGGL((gemm256_kernel<T, Epi>), dim3(tiles256), dim3(512), 0, s, (const T*)A,
-                       (const T*)W, M, N, K, epi);
+  if (N % 256 == 0 && variant != 128 && (tiles256 >= 256 || variant >= 256)) {
+    if (variant == 257)
+      hipLaunchKernelGGL((gemm256_kernel<T, Epi, 1>), dim3(tiles256), dim3(512), 0, s,
+                         (const T*)A, (const T*)W, M, N, K, epi);
+    else
+      hipLaunchKernelGGL((gemm256_kernel<T, Epi, 0>), dim3(tiles256), dim3(512), 0, s,
+                         (const T*)A, (const T*)W, M, N, K, epi);
     return hipGetLastError();
   }
   constexpr int BM = 128, BN = 128;

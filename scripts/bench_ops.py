@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--variants", default="128,256")
     ap.add_argument("--ops", default="gemm,attention,layernorm")
+    ap.add_argument("--ksweep", action="store_true", help="N=1024 GEMM at K=1024..8192")
     args = ap.parse_args()
     lib = _lib.load_library()
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -55,6 +56,8 @@ def main():
         X = torch.randn(M, W, device="cuda", generator=g)
         shapes = [("qkv", 3 * W, W, 0, 0), ("out", W, W, 1, 0), ("fc", 4 * W, W, 0, 1),
                   ("proj", W, 4 * W, 1, 0)]
+        if args.ksweep:
+            shapes = [(f"k{k}", 4 * W, k, 2, 0) for k in (256, 1024, 2048, 4096)]
         for v in [int(x) for x in args.variants.split(",")]:
             for name, N, K, epi, act in shapes:
                 C = X if epi == 1 else C16

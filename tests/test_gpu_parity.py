@@ -164,3 +164,22 @@ def test_module_surface():
     assert next(m.parameters()).device.type == "cuda"
     assert m.visual.input_resolution == 224 and m.dtype == torch.float16
     assert "visual.transformer.resblocks.11.mlp.c_proj.weight" in sd
+
+
+@pytest.mark.parametrize("B,C,k", [(13, 20, 5), (1, 7, 1), (64, 1000, 5)])
+def test_zero_shot_head_vs_torch(B, C, k):
+    """Batched head kernel (8 rows per workgroup, ragged tail) against torch fp32."""
+    m = _model("ViT-B/32", "fp16")
+    g = torch.Generator(device="cuda").manual_seed(B + C)
+    feats = torch.randn(B, 768, device="cuda", generator=g)
+    tw = torch.nn.functional.normalize(torch.randn(512, C, device="cuda", generator=g), dim=0)
+    logits, top = m.zero_shot(feats, tw, 100.0, k=k, apply_proj=True)
+    ref = 100.0 * torch.nn.functional.normalize(feats @ m.visual.proj, dim=-1) @ tw
+    assert (logits - ref).abs().max().item() < 2e-3
+    rv, ri = ref.topk(k, 1, True, True)
+    gap = (rv[:, :-1] - rv[:, 1:]).min().item() if k > 1 else 1.0
+    if gap > 1e-3:
+        assert torch.equal(top.cpu(), ri.cpu())
+    nf = torch.nn.functional.normalize(feats @ m.visual.proj, dim=-1)
+    l2, _ = m.zero_shot(nf, tw, 100.0, k=0, apply_proj=False)
+    assert (l2 - ref).abs().max().item() < 2e-3
