@@ -433,6 +433,122 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// 256x128x32 tile, 256 threads = 4 waves as 2(M) x 2(N), 128x64 per wave,
+// three LDS stages of 24 KiB (72 KiB per workgroup) so TWO workgroups share a
+// CU: one workgroup's prologue/epilogue (HBM-burst bound) overlaps the other's
+// MFMA main loop instead of idling the matrix pipes. 64-B LDS rows, 16-B
+// chunks swizzled by (row>>1)&3 (conflict-free 16x16x32 fragment reads under
+// the gfx950 ds_read_b128 lane groups). Prefetch distance two K-steps:
+// vmcnt(6) once per K-step (6 LDS-DMA per lane per stage).
+// ---------------------------------------------------------------------------
+template <typename T, class Epi>
+__global__ __launch_bounds__(256, 2) void gemm_t2_kernel(const T* __restrict__ A,
+                                                         const T* __restrict__ W, int M, int N,
+                                                         int K, Epi epi) {
+  constexpr int BM = 256, BN = 128, BKk = 32;
+  constexpr int A_BYTES = BM * 64, STAGE = (BM + BN) * 64;   // 16 KiB + 8 KiB
+  constexpr int EPI_LD = 132;
+  constexpr int SMEM = 3 * STAGE > 128 * EPI_LD * 4 ? 3 * STAGE : 128 * EPI_LD * 4;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int ntn = N / BN, ntm = (M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, ntm * ntn);
+  const int tm = bid / ntn, tn = bid - tm * ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // LDS-DMA: piece = 16 rows x 64 B; lane -> row lane>>2, physical chunk lane&3
+  const int lchunk = (lane & 3) ^ ((lane >> 3) & 3);
+  const T* asrc[4];
+  const T* bsrc[2];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    int r = m0 + (wave * 4 + p) * 16 + (lane >> 2);
+    r = r < M ? r : M - 1;
+    asrc[p] = A + (size_t)r * K + lchunk * 8;
+  }
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int c = n0 + (wave * 2 + p) * 16 + (lane >> 2);
+    bsrc[p] = W + (size_t)c * K + lchunk * 8;
+  }
+  auto stage = [&](int buf, int k0) {
+    char* sa = smem + buf * STAGE;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) glds16(asrc[p] + k0, sa + (wave * 4 + p) * 1024);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) glds16(bsrc[p] + k0, sa + A_BYTES + (wave * 2 + p) * 1024);
+  };
+
+  const int fr = lane & 15, fk = lane >> 4;
+  const int swz = (fk ^ ((fr >> 1) & 3)) << 4;
+  const int aoff = (wr * 128 + fr) * 64 + swz;
+  const int boff = A_BYTES + (wc * 64 + fr) * 64 + swz;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BKk;
+  stage(0, 0);
+  if (nk > 1) stage(1, BKk);
+  int cur = 0;
+  for (int t = 0; t < nk; ++t) {
+    if (t + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    if (t + 2 < nk) stage(cur == 0 ? 2 : cur - 1, (t + 2) * BKk);
+    const char* sb = smem + cur * STAGE;
+    i16x8 af[8], bf[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = *(const i16x8*)(sb + boff + j * 1024);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = *(const i16x8*)(sb + aoff + i * 1024);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = Mfma<T>::m16(af[i], bf[j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    cur = cur == 2 ? 0 : cur + 1;
+  }
+
+  // epilogue: two passes (wr), 128 rows x 128 cols fp32 staged, 512-B row reads
+  float* stg = (float*)smem;
+  const int ec = (tid & 31) * 4;
+  const float4 bv = epi.bias4(n0 + ec);
+  const bool full = m0 + BM <= M;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    lds_barrier();
+    if (wr == q) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            stg[(i * 16 + fk * 4 + r) * EPI_LD + wc * 64 + j * 16 + fr] = acc[i][j][r];
+    }
+    lds_barrier();
+#pragma unroll 4
+    for (int k = 0; k < 16; ++k) {
+      const int lr = (tid >> 5) + 8 * k;
+      const int row = m0 + q * 128 + lr;
+      const float4 v = *(const float4*)(stg + lr * EPI_LD + ec);
+      if (full || row < M) epi.put4(row, n0 + ec, v, bv);
+    }
+  }
+}
+
 // MICLIP_GEMM=128 forces the 128x128 kernel (A/B comparisons), 256 forces the
 // 256x256 one wherever the shape allows; default picks by problem size.
 int gemm_variant() {
@@ -452,8 +568,14 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
                   int variant = 0) {
   if (!gemm_shape_ok(M, N, K)) return hipErrorInvalidValue;
   if (variant == 0) variant = gemm_variant();
-  if (variant != 0 && variant != 128 && variant != 256 && variant != 257)
+  if (variant != 0 && variant != 128 && variant != 256 && variant != 257 && variant != 2)
     return hipErrorInvalidValue;
+  if (variant == 2) {   // 256x128, two workgroups per CU
+    const int tiles = ((M + 255) / 256) * (N / 128);
+    hipLaunchKernelGGL((gemm_t2_kernel<T, Epi>), dim3(tiles), dim3(256), 0, s, (const T*)A,
+                       (const T*)W, M, N, K, epi);
+    return hipGetLastError();
+  }
   // Large problems: 256x256 tile (1 WG/CU, L2-friendly arithmetic intensity);
   // small ones (text tower, tiny batches) keep more workgroups with 128x128.
   const int tiles256 = ((M + 255) / 256) * (N / 256);

@@ -33,7 +33,9 @@ def _check(lib, rc):
 @pytest.mark.parametrize("M,N,K,variant", [(300, 256, 192, 0), (128, 128, 64, 0), (65, 384, 1024, 0),
                                           (1000, 768, 3072, 128), (1000, 768, 3072, 256),
                                           (300, 256, 192, 256), (257, 512, 64, 256),
-                                          (4096, 1024, 1024, 0), (33, 2304, 768, 256)])
+                                          (4096, 1024, 1024, 0), (33, 2304, 768, 256),
+                                          (1000, 768, 3072, 2), (300, 256, 192, 2), (257, 512, 64, 2),
+                                          (33, 2304, 768, 257), (600, 1024, 4096, 257)])
 @pytest.mark.parametrize("epi,act", [(0, 0), (0, 1), (0, 2), (1, 0), (2, 0)])
 def test_gemm(lib, dt, M, N, K, variant, epi, act):
     code, tdt = DT[dt]
