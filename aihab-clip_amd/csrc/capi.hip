@@ -571,6 +571,8 @@ int miclip_op_gemm(int32_t dtype, const void* A, const void* W, const float* bia
     MICLIP_HIP(gemm_residual(dtype, A, W, bias, (float*)C, M, N, K, s, variant));
   } else if (epi == 2) {
     MICLIP_HIP(gemm_f32(dtype, A, W, bias, (float*)C, M, N, K, s, variant));
+  } else if (epi == 3) {
+    MICLIP_HIP(gemm_null(dtype, A, W, (float*)C, M, N, K, s, variant));
   } else {
     return fail(MICLIP_EINVAL, "unknown epilogue");
   }

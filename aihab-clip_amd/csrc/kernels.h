@@ -21,6 +21,9 @@ hipError_t gemm_residual(int dtype, const void* A, const void* W, const float* b
 // Float epilogue: C (fp32, ld = N) = acc + bias (bias may be null).
 hipError_t gemm_f32(int dtype, const void* A, const void* W, const float* bias, float* C,
                     int M, int N, int K, hipStream_t s, int variant = 0);
+// Diagnostic epilogue that writes nothing (prices the epilogue in A/B timing).
+hipError_t gemm_null(int dtype, const void* A, const void* W, float* C, int M, int N, int K,
+                     hipStream_t s, int variant = 0);
 // Patch-embed epilogue: row m = b*np + p of the patch GEMM goes to token row
 // b*(np+1) + 1 + p of X (fp32, ld = N), plus positional embedding row 1 + p.
 hipError_t gemm_patch(int dtype, const void* A, const void* W, const float* pos, float* X,

@@ -140,7 +140,7 @@ int miclip_profile_read(miclip_model* m, miclip_kernel_stat* out, int32_t n, int
 
 /* C = A[M,K] . W[N,K]^T + bias, A/W in compute dtype `dtype`.
  * epi 0: C dtype = act(.) with act from `act` (0 none); epi 1: C fp32 += (residual);
- * epi 2: C fp32 = . ; N % 128 == 0 and K % 64 == 0 required. variant: 0 = tile
+ * epi 2: C fp32 = . ; epi 3: no output (diagnostic: prices the epilogue); N % 128 == 0 and K % 64 == 0 required. variant: 0 = tile
  * chosen by size, 128 / 256 = force the 128x128 / 256x256 kernel (N % 256 for 256).
  * Replaces torch Linear (clip/model.py:171-175) and MHA in/out projections. */
 int miclip_op_gemm(int32_t dtype, const void* A, const void* W, const float* bias, void* C,

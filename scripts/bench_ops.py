@@ -57,7 +57,7 @@ def main():
         shapes = [("qkv", 3 * W, W, 0, 0), ("out", W, W, 1, 0), ("fc", 4 * W, W, 0, 1),
                   ("proj", W, 4 * W, 1, 0)]
         if args.ksweep:
-            shapes = [(f"k{k}", 4 * W, k, 2, 0) for k in (256, 1024, 2048, 4096)]
+            shapes = [(f"k{k}_e{e}", 4 * W, k, e, 0) for e in (3, 0, 2) for k in (256, 1024, 4096)]
         for v in [int(x) for x in args.variants.split(",")]:
             for name, N, K, epi, act in shapes:
                 C = X if epi == 1 else C16
@@ -68,7 +68,7 @@ def main():
                     assert rc == 0, lib.miclip_last_error()
                 ms = timeit(fn, args.iters)
                 fl = 2.0 * M * N * K
-                by = 2.0 * M * K + 2.0 * N * K + (8.0 if epi == 1 else 2.0) * M * N
+                by = 2.0 * M * K + 2.0 * N * K + {0: 2.0, 1: 8.0, 2: 4.0, 3: 0.0}[epi] * M * N
                 out.append(dict(op=f"gemm_{name}", variant=v, M=M, N=N, K=K, ms=round(ms, 4),
                                 tflops=round(fl / ms / 1e9, 1), gbs=round(by / ms / 1e6, 1)))
                 print(json.dumps(out[-1]), flush=True)
