@@ -263,9 +263,8 @@ MICLIP_DEV void lds_barrier() {
 }
 
 // SCHED 0: the half-tile schedule above (4 barriers per K-tile, ~1.5 K-tiles
-// in flight). SCHED 1: one barrier per K-tile; right after it the whole next
-// K-tile is issued (8 LDS-DMA per lane) and the 4 quadrant phases run without
-// barriers, so the compiler can pipeline fragment reads under the MFMAs.
+// in flight, fragment reads right after each barrier). SCHED 1: fragment
+// prefetch one quadrant ahead, one barrier per K-tile (see the branch below).
 template <typename T, class Epi, int SCHED>
 __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
                                                       const T* __restrict__ W, int M, int N,
@@ -384,32 +383,71 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
       }
     }
   } else {
-    stage(0, 0);
-    stage(2, 0);
-    stage(3, 0);
-    stage(1, 0);
+    // Fragment-prefetch schedule: all four fragment sets live (A0/A1 32 VGPRs,
+    // B0/B1 16 each); each set is read from LDS one quadrant before its first
+    // MFMA, so LDS reads run under the previous quadrant's MFMAs. Quadrant order
+    // Q0=(A0,B0) Q1=(A0,B1) Q2=(A1,B0) Q3=(A1,B1) frees A0 after Q1 and B0 after
+    // Q2, where the next K-tile's A0/B0 are prefetched. One barrier per K-tile
+    // (mid-tile): it retires the next K-tile's LDS-DMA (RAW) and every read of
+    // this K-tile's buffer (WAR) before the K-tile after next is issued into it.
+    i16x8 a0[2][4], a1[2][4], b0[2][2], b1[2][2];
+    auto rdA = [&](i16x8 (&d)[2][4], const char* sa) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        d[0][i] = *(const i16x8*)(sa + i * 2048 + sw0);
+        d[1][i] = *(const i16x8*)(sa + i * 2048 + sw1);
+      }
+    };
+    auto rdB = [&](i16x8 (&d)[2][2], const char* sb) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        d[0][j] = *(const i16x8*)(sb + j * 2048 + sw0);
+        d[1][j] = *(const i16x8*)(sb + j * 2048 + sw1);
+      }
+    };
+    auto mm = [&](const i16x8 (&a)[2][4], const i16x8 (&b)[2][2], int qi, int qj) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[qi][qj][i][j] = Mfma<T>::m16(a[s][i], b[s][j], acc[qi][qj][i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    auto stage_all = [&](int tile) {
+      stage(0, tile);
+      stage(2, tile);
+      stage(1, tile);
+      stage(3, tile);
+    };
+    auto slot = [&](int buf, int kind) -> const char* {
+      return smem + (buf * 4 + kind) * HALF + (kind < 2 ? aoff : boff);
+    };
+    stage_all(0);
+    if (nk > 1) {
+      stage_all(1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_barrier();
+    rdA(a0, slot(0, 0));
+    rdB(b0, slot(0, 2));
     for (int t = 0; t < nk; ++t) {
       const int buf = t & 1;
-      const char* sA0 = smem + (buf * 4 + 0) * HALF + aoff;
-      const char* sA1 = smem + (buf * 4 + 1) * HALF + aoff;
-      const char* sB0 = smem + (buf * 4 + 2) * HALF + boff;
-      const char* sB1 = smem + (buf * 4 + 3) * HALF + boff;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      rdB(b1, slot(buf, 3));
+      rdA(a1, slot(buf, 1));
+      mm(a0, b0, 0, 0);
+      mm(a0, b1, 0, 1);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       lds_barrier();
-      if (t + 1 < nk) {
-        stage(0, t + 1);
-        stage(2, t + 1);
-        stage(3, t + 1);
-        stage(1, t + 1);
-      }
-      quadrant(sA0, sB0, 0, 0, true);
-      mfma_q(0, 0);
-      quadrant(sA0, sB1, 0, 1, false);
-      mfma_q(0, 1);
-      quadrant(sA1, sB1, 1, 1, true);
-      mfma_q(1, 1);
-      quadrant(sA1, sB0, 1, 0, false);
-      mfma_q(1, 0);
+      if (t + 2 < nk) stage_all(t + 2);
+      if (t + 1 < nk) rdA(a0, slot(buf ^ 1, 0));
+      mm(a1, b0, 1, 0);
+      if (t + 1 < nk) rdB(b0, slot(buf ^ 1, 2));
+      mm(a1, b1, 1, 1);
     }
   }
 
