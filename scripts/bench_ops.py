@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--variants", default="128,256")
     ap.add_argument("--ops", default="gemm,attention,layernorm")
     ap.add_argument("--ksweep", action="store_true", help="N=1024 GEMM at K=1024..8192")
+    ap.add_argument("--only", default="", help="comma list of gemm shape names to run")
     args = ap.parse_args()
     lib = _lib.load_library()
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -58,6 +59,8 @@ def main():
                   ("proj", W, 4 * W, 1, 0)]
         if args.ksweep:
             shapes = [(f"k{k}_e{e}", 4 * W, k, e, 0) for e in (3, 0, 2) for k in (256, 1024, 4096)]
+        if args.only:
+            shapes = [sh for sh in shapes if sh[0] in args.only.split(",")]
         for v in [int(x) for x in args.variants.split(",")]:
             for name, N, K, epi, act in shapes:
                 C = X if epi == 1 else C16
