@@ -476,16 +476,224 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
             stg[lr * EPI_LD + lc] = acc[qi][qj][i][j][r];
           }
     lds_barrier();
+    if (full) {
 #pragma unroll 4
-    for (int k = 0; k < 16; ++k) {
-      const int lr = (tid >> 6) + 8 * k;                      // 0..127
-      const int row = m0 + (lr >> 6) * 128 + qi * 64 + (lr & 63);
-      const float4 v = *(const float4*)(stg + lr * EPI_LD + ec);
-      if (full || row < M) epi.put4(row, n0 + ec, v, bv);
+      for (int k = 0; k < 16; ++k) {
+        const int lr = (tid >> 6) + 8 * k;                      // 0..127
+        const int row = m0 + (lr >> 6) * 128 + qi * 64 + (lr & 63);
+        epi.put4(row, n0 + ec, *(const float4*)(stg + lr * EPI_LD + ec), bv);
+      }
+    } else {
+#pragma unroll 4
+      for (int k = 0; k < 16; ++k) {
+        const int lr = (tid >> 6) + 8 * k;
+        const int row = m0 + (lr >> 6) * 128 + qi * 64 + (lr & 63);
+        if (row < M) epi.put4(row, n0 + ec, *(const float4*)(stg + lr * EPI_LD + ec), bv);
+      }
     }
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Persistent form of the 256x256 SCHED-0 kernel: one workgroup per CU walks
+// its tiles (XCD-contiguous round robin) as ONE continuous K-step stream, so
+// the half-tile LDS-DMA pipeline runs straight across tile boundaries (no
+// per-tile prologue bubble) and a tile's epilogue stores drain while the next
+// tile's first K-steps load and compute.
+//   LDS: 128 KiB pipeline (2 buffers x {A0,A1,B0,B1}) + 32 KiB epilogue
+//   region X. At a tile's last K-step the slots A1/B0 of the current buffer
+//   are free until the next K-step's phases 0/1 restage them, so they form
+//   epilogue region Y; the epilogue runs 8 passes of 32 rows alternating
+//   X / Y, one barrier per pass.
+//   vmcnt at phase 0 of a K-step that follows an epilogue: the only ops
+//   younger than that K-step's data are A0/B1 of the step after it (4) and the
+//   epilogue's 32 stores (+ loads, already retired when consumed), so
+//   vmcnt(36) retires exactly the needed data; otherwise vmcnt(4).
+// ---------------------------------------------------------------------------
+template <typename T, class Epi>
+__global__ __launch_bounds__(512) void gemm256p_kernel(const T* __restrict__ A,
+                                                       const T* __restrict__ W, int M, int N,
+                                                       int K, Epi epi) {
+  constexpr int HALF = 128 * 128;
+  constexpr int EPI_LD = 256;   // 32 rows x 256 fp32 = 32 KiB per pass, no pad
+  __shared__ __attribute__((aligned(1024))) char smem[8 * HALF + 32 * 1024];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int ntn = N / 256, ntm = (M + 255) / 256, ntiles = ntm * ntn;
+  const int G = gridDim.x;
+  // XCD-contiguous assignment: round j, XCD x = blockIdx % 8, slot q = blockIdx / 8
+  const int gx = G / 8 > 0 ? G / 8 : 1;
+  const int xcd = blockIdx.x % 8, q = blockIdx.x / 8;
+  const int first = (G % 8 == 0) ? xcd * gx + q : blockIdx.x;
+  const int my_tiles = first < ntiles ? (ntiles - 1 - first) / G + 1 : 0;
+  const int nk = K / 64;
+  const int S = my_tiles * nk;
+  if (S == 0) return;
+
+  // per-lane LDS-DMA geometry: slot row sr = wave*16 + 8*pp + (lane>>3); the
+  // element offsets fit 32 bits (launcher checks M*K, N*K < 2^31)
+  const int lchunk8 = ((lane & 7) ^ (lane >> 3)) * 8;
+  int arow[2][2], bcol[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      const int sr = wave * 16 + 8 * pp + (lane >> 3);
+      arow[h][pp] = (sr >> 6) * 128 + h * 64 + (sr & 63);
+      bcol[h][pp] = (sr >> 5) * 64 + h * 32 + (sr & 31);
+    }
+  auto stage = [&](int kind, int step) {
+    const int j = step / nk, kt = step - j * nk;
+    const int tile = first + j * G;
+    const int tm = tile / ntn;
+    const int m0 = tm * 256, n0 = (tile - tm * ntn) * 256;
+    char* dst = smem + ((step & 1) * 4 + kind) * HALF + wave * 2048;
+    const int h = kind & 1;
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      if (kind < 2) {
+        int r = m0 + arow[h][pp];
+        r = r < M ? r : M - 1;
+        glds16(A + (unsigned)(r * K + kt * 64 + lchunk8), dst + pp * 1024);
+      } else {
+        glds16(W + (unsigned)((n0 + bcol[h][pp]) * K + kt * 64 + lchunk8), dst + pp * 1024);
+      }
+    }
+  };
+  // kind: 0 A0, 1 A1, 2 B0, 3 B1  (stage(kind) uses h = kind&1: A0/B0 h=0, A1/B1 h=1)
+
+  const int fr = lane & 15, fk = lane >> 4;
+  const int aoff = (wr * 64 + fr) * 128, boff = (wc * 32 + fr) * 128;
+  const int sw0 = ((0 + fk) ^ (fr & 7)) << 4, sw1 = ((4 + fk) ^ (fr & 7)) << 4;
+
+  f32x4 acc[2][2][4][2];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  zero_acc();
+
+  stage(0, 0);
+  stage(3, 0);
+  stage(1, 0);
+  stage(2, 0);
+  if (S > 1) {
+    stage(0, 1);
+    stage(3, 1);
+  }
+
+  i16x8 af[2][4], bf[2][2];
+  bool after_epi = false;
+  for (int st = 0; st < S; ++st) {
+    const int buf = st & 1;
+    const char* sA0 = smem + (buf * 4 + 0) * HALF + aoff;
+    const char* sA1 = smem + (buf * 4 + 1) * HALF + aoff;
+    const char* sB0 = smem + (buf * 4 + 2) * HALF + boff;
+    const char* sB1 = smem + (buf * 4 + 3) * HALF + boff;
+    if (st + 1 >= S)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (after_epi)
+      asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      lds_barrier();
+      const int qi = (p >= 2) ? 1 : 0;
+      const int qj = (p == 1 || p == 2) ? 1 : 0;
+      if (p == 0 || p == 2) {
+        const char* sa = qi ? sA1 : sA0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          af[0][i] = *(const i16x8*)(sa + i * 2048 + sw0);
+          af[1][i] = *(const i16x8*)(sa + i * 2048 + sw1);
+        }
+      }
+      {
+        const char* sb = qj ? sB1 : sB0;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          bf[0][j] = *(const i16x8*)(sb + j * 2048 + sw0);
+          bf[1][j] = *(const i16x8*)(sb + j * 2048 + sw1);
+        }
+      }
+      if (p == 0 && st + 1 < S) stage(1, st + 1);
+      if (p == 1 && st + 1 < S) stage(2, st + 1);
+      if (p == 2 && st + 2 < S) stage(0, st + 2);
+      if (p == 3 && st + 2 < S) stage(3, st + 2);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[qi][qj][i][j] = Mfma<T>::m16(af[s2][i], bf[s2][j], acc[qi][qj][i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    after_epi = false;
+    if (st - (st / nk) * nk != nk - 1) continue;
+
+    // ---- epilogue of the tile that just finished ----
+    const int tile = first + (st / nk) * G;
+    const int m0 = (tile / ntn) * 256, n0 = (tile - (tile / ntn) * ntn) * 256;
+    const int ec = (tid & 63) * 4;
+    const float4 bv = epi.bias4(n0 + ec);
+    const bool full = m0 + 256 <= M;
+    float* regX = (float*)(smem + 8 * HALF);
+    float* regY = (float*)(smem + (buf * 4 + 1) * HALF);
+#pragma unroll
+    for (int pass = 0; pass < 8; ++pass) {
+      float* stg = (pass & 1) ? regY : regX;
+      const int pwr = pass >> 2, pqi = (pass >> 1) & 1, pi0 = (pass & 1) * 2;
+      if (wr == pwr) {
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int lr = ii * 16 + fk * 4 + r;
+                const int lc = wc * 64 + qj * 32 + j * 16 + fr;
+                stg[lr * EPI_LD + (lc ^ ((lr & 7) << 2))] = acc[pqi][qj][pi0 + ii][j][r];
+              }
+      }
+      lds_barrier();
+      // branch-free store loop for full tiles: a store under a per-row branch
+      // makes hipcc wait vmcnt(0) before every store (guide §5, trap 4(c))
+      if (full) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int lr = (tid >> 6) + 8 * k;                    // 0..31
+          const int row = m0 + pwr * 128 + pqi * 64 + pi0 * 16 + lr;
+          const float4 v = *(const float4*)(stg + lr * EPI_LD + (ec ^ ((lr & 7) << 2)));
+          epi.put4(row, n0 + ec, v, bv);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int lr = (tid >> 6) + 8 * k;
+          const int row = m0 + pwr * 128 + pqi * 64 + pi0 * 16 + lr;
+          const float4 v = *(const float4*)(stg + lr * EPI_LD + (ec ^ ((lr & 7) << 2)));
+          if (row < M) epi.put4(row, n0 + ec, v, bv);
+        }
+      }
+    }
+    zero_acc();
+    after_epi = true;
+  }
+}
 
 // ---------------------------------------------------------------------------
 // 256x128x32 tile, 256 threads = 4 waves as 2(M) x 2(N), 128x64 per wave,
@@ -621,8 +829,25 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
                   int variant = 0) {
   if (!gemm_shape_ok(M, N, K)) return hipErrorInvalidValue;
   if (variant == 0) variant = gemm_variant();
-  if (variant != 0 && variant != 128 && variant != 256 && variant != 257 && variant != 2)
+  if (variant != 0 && variant != 128 && variant != 256 && variant != 257 && variant != 2 &&
+      variant != 3)
     return hipErrorInvalidValue;
+  if (variant == 3) {   // persistent 256x256
+    static int ncu = [] {
+      int d = 0, n = 0;
+      if (hipGetDevice(&d) != hipSuccess ||
+          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+        n = 256;
+      return n;
+    }();
+    const int tiles = ((M + 255) / 256) * (N / 256);
+    if (N % 256 == 0 && (long long)M * K < (1ll << 31) && (long long)N * K < (1ll << 31)) {
+      const int grid = tiles < ncu ? tiles : ncu;
+      hipLaunchKernelGGL((gemm256p_kernel<T, Epi>), dim3(grid), dim3(512), 0, s, (const T*)A,
+                         (const T*)W, M, N, K, epi);
+      return hipGetLastError();
+    }
+  }
   if (variant == 2) {   // 256x128, two workgroups per CU
     const int tiles = ((M + 255) / 256) * (N / 128);
     hipLaunchKernelGGL((gemm_t2_kernel<T, Epi>), dim3(tiles), dim3(256), 0, s, (const T*)A,
