@@ -349,7 +349,65 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
     __builtin_amdgcn_s_setprio(0);
   };
 
-  if constexpr (SCHED == 0) {
+  if constexpr (SCHED == 2) {
+    // Staggered SCHED 0 (cdna_hip_programming.md §5 "256^2 8-phase template",
+    // its `if (wr == 1) s_barrier`): each phase is [R: fragment reads + one
+    // half-tile LDS-DMA + lgkmcnt(0)] barrier [M: 16 MFMAs] barrier, and waves
+    // 4-7 (wr = 1, the partners of waves 0-3 on the same SIMDs) run one barrier
+    // behind, so on every SIMD one wave reads LDS while its partner issues
+    // MFMAs. Hazards, in barrier intervals (group 0 does R_j in interval 2j,
+    // group 1 in 2j+1): every slot is restaged at least one interval after its
+    // last read by either group; group 0 retires its LDS-DMA up to B0(t+1) with
+    // vmcnt(4) at R of phase 0 of tile t+1, group 1 with vmcnt(2) at R of phase 3
+    // of tile t, each before the barrier that precedes the other group's reads.
+    stage(0, 0);
+    stage(3, 0);
+    stage(1, 0);
+    stage(2, 0);
+    if (nk > 1) {
+      stage(0, 1);
+      stage(3, 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_barrier();
+    if (wr == 1) lds_barrier();   // stagger (wr is wave-uniform: readfirstlane)
+    for (int t = 0; t < nk; ++t) {
+      const int buf = t & 1;
+      const char* sA0 = smem + (buf * 4 + 0) * HALF + aoff;
+      const char* sA1 = smem + (buf * 4 + 1) * HALF + aoff;
+      const char* sB0 = smem + (buf * 4 + 2) * HALF + boff;
+      const char* sB1 = smem + (buf * 4 + 3) * HALF + boff;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        if (p == 0 && wr == 0 && t > 0) {
+          if (t + 1 < nk)
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (p == 3 && wr == 1 && t + 1 < nk) {
+          if (t + 2 < nk)
+            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const int qi = (p >= 2) ? 1 : 0;
+        const int qj = (p == 1 || p == 2) ? 1 : 0;
+        quadrant(qi ? sA1 : sA0, qj ? sB1 : sB0, qi, qj, p == 0 || p == 2);
+        if (p == 0 && t + 1 < nk) stage(1, t + 1);
+        if (p == 1 && t + 1 < nk) stage(2, t + 1);
+        if (p == 2 && t + 2 < nk) stage(0, t + 2);
+        if (p == 3 && t + 2 < nk) stage(3, t + 2);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        lds_barrier();
+        mfma_q(qi, qj);
+        lds_barrier();
+      }
+    }
+    if (wr == 0) lds_barrier();   // balance the stagger barrier
+  } else if constexpr (SCHED == 0) {
     // prologue: A0(0) B1(0) A1(0) B0(0) A0(1) B1(1)
     stage(0, 0);
     stage(3, 0);
@@ -829,8 +887,8 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
                   int variant = 0) {
   if (!gemm_shape_ok(M, N, K)) return hipErrorInvalidValue;
   if (variant == 0) variant = gemm_variant();
-  if (variant != 0 && variant != 128 && variant != 256 && variant != 257 && variant != 2 &&
-      variant != 3)
+  if (variant != 0 && variant != 128 && variant != 256 && variant != 257 && variant != 258 &&
+      variant != 2 && variant != 3)
     return hipErrorInvalidValue;
   if (variant == 3) {   // persistent 256x256
     static int ncu = [] {
@@ -860,6 +918,9 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   if (N % 256 == 0 && variant != 128 && (tiles256 >= 256 || variant >= 256)) {
     if (variant == 257)
       hipLaunchKernelGGL((gemm256_kernel<T, Epi, 1>), dim3(tiles256), dim3(512), 0, s,
+                         (const T*)A, (const T*)W, M, N, K, epi);
+    else if (variant == 258)
+      hipLaunchKernelGGL((gemm256_kernel<T, Epi, 2>), dim3(tiles256), dim3(512), 0, s,
                          (const T*)A, (const T*)W, M, N, K, epi);
     else
       hipLaunchKernelGGL((gemm256_kernel<T, Epi, 0>), dim3(tiles256), dim3(512), 0, s,

@@ -21,8 +21,8 @@ for step in "${steps[@]}"; do
     gpu)     run gputests 1000 python -m pytest tests -m gpu -q -rf ;;
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   run bench 600 python bench.py --steps 10 --warmup 3 ;;
-    ops)     run ops 300 python scripts/bench_ops.py --variants 256,3,256,3 ;;
-    ksweep)  run ksweep 300 python scripts/bench_ops.py --variants 256,3 --ksweep --ops gemm ;;
+    ops)     run ops 300 python scripts/bench_ops.py --variants 256,258,256,258 ;;
+    ksweep)  run ksweep 300 python scripts/bench_ops.py --variants 256,258 --ksweep --ops gemm ;;
     prof)    export TMPDIR=/tmp
              run prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
                  -d "$PWD/gpurun_out/prof" -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
