@@ -916,14 +916,15 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   // small ones (text tower, tiny batches) keep more workgroups with 128x128.
   const int tiles256 = ((M + 255) / 256) * (N / 256);
   if (N % 256 == 0 && variant != 128 && (tiles256 >= 256 || variant >= 256)) {
+    // default: the staggered schedule (SCHED 2); 256 / 257 select SCHED 0 / 1
     if (variant == 257)
       hipLaunchKernelGGL((gemm256_kernel<T, Epi, 1>), dim3(tiles256), dim3(512), 0, s,
                          (const T*)A, (const T*)W, M, N, K, epi);
-    else if (variant == 258)
-      hipLaunchKernelGGL((gemm256_kernel<T, Epi, 2>), dim3(tiles256), dim3(512), 0, s,
+    else if (variant == 256)
+      hipLaunchKernelGGL((gemm256_kernel<T, Epi, 0>), dim3(tiles256), dim3(512), 0, s,
                          (const T*)A, (const T*)W, M, N, K, epi);
     else
-      hipLaunchKernelGGL((gemm256_kernel<T, Epi, 0>), dim3(tiles256), dim3(512), 0, s,
+      hipLaunchKernelGGL((gemm256_kernel<T, Epi, 2>), dim3(tiles256), dim3(512), 0, s,
                          (const T*)A, (const T*)W, M, N, K, epi);
     return hipGetLastError();
   }
