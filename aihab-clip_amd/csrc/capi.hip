@@ -116,6 +116,9 @@ struct miclip_model {
   float* text_proj = nullptr;
   float* logit_scale = nullptr;
   Workspace wimg, wtxt;
+  int splits = 2;               // batch split over the caller stream + aux (miclip_set_splits)
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // per-kernel-class HIP-event timing (miclip_set_profiling)
   struct ProfRec {
     int cls;
@@ -295,6 +298,71 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
   return 0;
 }
 
+// A window of the workspace: rows [row0, ...) / items [item0, ...).
+Workspace view(const miclip_model* m, const Workspace& w, size_t row0, size_t item0, int N,
+               int W) {
+  Workspace v = w;
+  const size_t e = elt();
+  const int g = m->cfg.image_resolution / m->cfg.vision_patch_size;
+  if (w.patches) v.patches = (char*)w.patches + item0 * g * g * m->Kp * e;
+  v.x = w.x + row0 * W;
+  v.h = (char*)w.h + row0 * W * e;
+  v.qkv = (char*)w.qkv + row0 * 3 * W * e;
+  v.o = (char*)w.o + row0 * W * e;
+  v.f = (char*)w.f + row0 * 4 * W * e;
+  v.feat = w.feat + item0 * W;
+  v.rows = w.rows + item0;
+  (void)N;
+  return v;
+}
+
+int ensure_aux(miclip_model* m) {
+  if (m->aux) return 0;
+  MICLIP_HIP(hipStreamCreateWithFlags(&m->aux, hipStreamNonBlocking));
+  MICLIP_HIP(hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming));
+  MICLIP_HIP(hipEventCreateWithFlags(&m->ev_join, hipEventDisableTiming));
+  return 0;
+}
+
+// encode_image for B images whose workspace window is `w` (clip/model.py:216-235)
+int encode_image_part(miclip_model* m, Workspace w, const float* images, int B, float* out,
+                      uint32_t flags, hipStream_t s) {
+  const auto& c = m->cfg;
+  const int P = c.vision_patch_size, R = c.image_resolution, W = c.vision_width;
+  const int g = R / P, np = g * g, N = np + 1, H = W / 64, dt = m->dtype;
+  const int M = B * N;
+  int rc;
+  {
+    ProfScope p(m, K_IM2COL, s, 0, (double)B * 3 * R * R * 4 + (double)B * np * m->Kp * 2);
+    MICLIP_HIP(im2col(dt, images, w.patches, B, R, P, m->Kp, s));
+  }
+  {
+    const double dM = (double)B * np;
+    ProfScope p(m, K_GEMM_PATCH, s, gemm_flops(dM, W, 3.0 * P * P), gemm_bytes(dM, W, m->Kp, 4));
+    MICLIP_HIP(gemm_patch(dt, w.patches, m->conv_w, m->vpos, w.x, B * np, W, m->Kp, np, s));
+  }
+  {
+    ProfScope p(m, K_LAYERNORM, s, 0, (double)M * W * 8);
+    MICLIP_HIP(class_token(m->cls, m->vpos, w.x, B, N, W, s));
+    MICLIP_HIP(layernorm(dt, w.x, nullptr, 1, m->ln_pre_g, m->ln_pre_b, w.x, nullptr, M, W, 0, s));
+  }
+  for (int l = 0; l < c.vision_layers; ++l)
+    if ((rc = run_block(m, m->vblocks[l], w, B, N, W, H, 0, s))) return rc;
+  const bool proj = flags & MICLIP_FLAG_APPLY_PROJ, norm = flags & MICLIP_FLAG_NORMALIZE;
+  // ln_post on the CLS rows only (clip/model.py:228): rows b*N
+  ProfScope p(m, K_HEAD, s, proj ? 2.0 * B * W * c.embed_dim : 0.0, (double)B * W * 8);
+  if (!proj) {
+    MICLIP_HIP(layernorm(dt, w.x, nullptr, N, m->ln_post_g, m->ln_post_b, out, nullptr, B, W,
+                         norm ? 1 : 0, s));
+  } else {
+    MICLIP_HIP(layernorm(dt, w.x, nullptr, N, m->ln_post_g, m->ln_post_b, w.feat, nullptr, B, W,
+                         0, s));
+    MICLIP_HIP(rowvec_matmul(w.feat, m->vproj, out, B, W, c.embed_dim, s));
+    if (norm) MICLIP_HIP(row_l2norm(out, B, c.embed_dim, s));
+  }
+  return 0;
+}
+
 bool cfg_ok(const miclip_config& c, std::string& why) {
   auto bad = [&](const char* w) { why = w; return false; };
   if (c.vision_width % 256 || c.vision_width < 256 || c.vision_width > 1536)
@@ -436,40 +504,35 @@ int miclip_encode_image(miclip_model* m, const float* images, int32_t B, float* 
     return fail(MICLIP_ENOWEIGHTS, "visual weights not loaded (missing " + missing(m, true) + ")");
   hipStream_t s = (hipStream_t)stream;
   const auto& c = m->cfg;
-  const int P = c.vision_patch_size, R = c.image_resolution, W = c.vision_width;
-  const int g = R / P, np = g * g, N = np + 1, H = W / 64, dt = m->dtype;
+  const int R = c.image_resolution, W = c.vision_width;
+  const int g = R / c.vision_patch_size, N = g * g + 1;
   int rc;
   if ((rc = ensure_ws(m, m->wimg, B, N, W, true))) return rc;
-  Workspace& w = m->wimg;
-  const int M = B * N;
-  {
-    ProfScope p(m, K_IM2COL, s, 0, (double)B * 3 * R * R * 4 + (double)B * np * m->Kp * 2);
-    MICLIP_HIP(im2col(dt, images, w.patches, B, R, P, m->Kp, s));
-  }
-  {
-    const double dM = (double)B * np;
-    ProfScope p(m, K_GEMM_PATCH, s, gemm_flops(dM, W, 3.0 * P * P), gemm_bytes(dM, W, m->Kp, 4));
-    MICLIP_HIP(gemm_patch(dt, w.patches, m->conv_w, m->vpos, w.x, B * np, W, m->Kp, np, s));
-  }
-  {
-    ProfScope p(m, K_LAYERNORM, s, 0, (double)M * W * 8);
-    MICLIP_HIP(class_token(m->cls, m->vpos, w.x, B, N, W, s));
-    MICLIP_HIP(layernorm(dt, w.x, nullptr, 1, m->ln_pre_g, m->ln_pre_b, w.x, nullptr, M, W, 0, s));
-  }
-  for (int l = 0; l < c.vision_layers; ++l)
-    if ((rc = run_block(m, m->vblocks[l], w, B, N, W, H, 0, s))) return rc;
-  const bool proj = flags & MICLIP_FLAG_APPLY_PROJ, norm = flags & MICLIP_FLAG_NORMALIZE;
-  // ln_post on the CLS rows only (clip/model.py:228): rows b*N
-  ProfScope p(m, K_HEAD, s, proj ? 2.0 * B * W * c.embed_dim : 0.0, (double)B * W * 8);
-  if (!proj) {
-    MICLIP_HIP(layernorm(dt, w.x, nullptr, N, m->ln_post_g, m->ln_post_b, out, nullptr, B, W,
-                         norm ? 1 : 0, s));
-  } else {
-    MICLIP_HIP(layernorm(dt, w.x, nullptr, N, m->ln_post_g, m->ln_post_b, w.feat, nullptr, B, W,
-                         0, s));
-    MICLIP_HIP(rowvec_matmul(w.feat, m->vproj, out, B, W, c.embed_dim, s));
-    if (norm) MICLIP_HIP(row_l2norm(out, B, c.embed_dim, s));
-  }
+  const int dim = (flags & MICLIP_FLAG_APPLY_PROJ) ? c.embed_dim : W;
+  // Batch split over two streams: the halves are independent images, so their
+  // kernel sequences can overlap (one half's HBM-bound epilogues / LayerNorm /
+  // attention run beside the other half's MFMA-bound GEMMs, and each GEMM's
+  // partial last wave of tiles is filled by the other stream's work).
+  const int splits = (m->splits > 1 && B >= 32 && !m->profiling) ? 2 : 1;
+  if (splits == 1) return encode_image_part(m, view(m, m->wimg, 0, 0, N, W), images, B, out, flags, s);
+  if ((rc = ensure_aux(m))) return rc;
+  const int b1 = (B + 1) / 2;
+  MICLIP_HIP(hipEventRecord(m->ev_fork, s));
+  MICLIP_HIP(hipStreamWaitEvent(m->aux, m->ev_fork, 0));
+  if ((rc = encode_image_part(m, view(m, m->wimg, 0, 0, N, W), images, b1, out, flags, s)))
+    return rc;
+  if ((rc = encode_image_part(m, view(m, m->wimg, (size_t)b1 * N, b1, N, W),
+                              images + (size_t)b1 * 3 * R * R, B - b1, out + (size_t)b1 * dim,
+                              flags, m->aux)))
+    return rc;
+  MICLIP_HIP(hipEventRecord(m->ev_join, m->aux));
+  MICLIP_HIP(hipStreamWaitEvent(s, m->ev_join, 0));
+  return 0;
+}
+
+int miclip_set_splits(miclip_model* m, int32_t splits) {
+  if (!m || splits < 1) return fail(MICLIP_EINVAL, "splits must be >= 1");
+  m->splits = splits;
   return 0;
 }
 
@@ -553,6 +616,9 @@ void miclip_model_destroy(miclip_model* m) {
     (void)hipEventDestroy(r.b);
   }
   for (hipEvent_t e : m->event_pool) (void)hipEventDestroy(e);
+  if (m->ev_fork) (void)hipEventDestroy(m->ev_fork);
+  if (m->ev_join) (void)hipEventDestroy(m->ev_join);
+  if (m->aux) (void)hipStreamDestroy(m->aux);
   for (auto& kv : m->allocs) (void)hipFree(kv.first);
   delete m;
 }

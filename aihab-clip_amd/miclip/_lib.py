@@ -21,7 +21,7 @@ EXPORTS = (
     "miclip_model_create", "miclip_model_load_weights", "miclip_reserve",
     "miclip_encode_image", "miclip_encode_text", "miclip_zero_shot",
     "miclip_model_destroy", "miclip_last_error", "miclip_abi_version",
-    "miclip_model_bytes", "miclip_set_profiling", "miclip_profile_read",
+    "miclip_model_bytes", "miclip_set_profiling", "miclip_profile_read", "miclip_set_splits",
     "miclip_op_gemm", "miclip_op_layernorm", "miclip_op_attention",
 )
 
@@ -73,6 +73,7 @@ def load_library(path: str = None):
         "miclip_abi_version": ([], ctypes.c_int),
         "miclip_model_bytes": ([vp], i64),
         "miclip_set_profiling": ([vp, ctypes.c_int], ctypes.c_int),
+        "miclip_set_splits": ([vp, i32], ctypes.c_int),
         "miclip_profile_read": ([vp, ctypes.POINTER(MiclipKernelStat), i32, i32], ctypes.c_int),
         "miclip_op_gemm": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp], ctypes.c_int),
         "miclip_op_layernorm": ([i32, vp, vp, vp, vp, i32, i32, i32, vp], ctypes.c_int),

@@ -161,6 +161,11 @@ class CLIP(nn.Module):
         h = self._require()
         _lib.check(h.lib.miclip_reserve(h.ptr, int(max_images), int(max_prompts)), "miclip_reserve")
 
+    def set_splits(self, splits=2):
+        """Split encode_image batches over 2 HIP streams (default) or not (1)."""
+        h = self._require()
+        _lib.check(h.lib.miclip_set_splits(h.ptr, int(splits)), "miclip_set_splits")
+
     def set_profiling(self, enable=True):
         h = self._require()
         _lib.check(h.lib.miclip_set_profiling(h.ptr, int(bool(enable))), "miclip_set_profiling")

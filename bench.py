@@ -88,6 +88,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--splits", type=int, default=2, help="encode_image batch split over streams")
+    ap.add_argument("--ab-splits", action="store_true", help="also time splits=1 vs 2 (diagnostic)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -107,6 +109,7 @@ def main():
     t_load = time.perf_counter()
     _, model, _ = miclip.load(args.model, device=dev, compute_dtype=args.dtype)
     model.reserve(B, args.classes)
+    model.set_splits(args.splits)
     log(f"[rank {rank}] model loaded in {time.perf_counter() - t_load:.1f}s")
 
     # synthetic CLIP-normalised images, device-resident before timing
@@ -157,6 +160,19 @@ def main():
     dt = float(dt_t.item())
     value = world * B * args.steps / dt
     gf = algorithmic_gflop_per_image(cfg)
+
+    ab = None
+    if args.ab_splits:
+        ab = {}
+        for sp in (1, 2, 1, 2):
+            model.set_splits(sp)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+            ab.setdefault(f"splits{sp}", []).append(round(world * B * args.steps / (time.perf_counter() - t1), 1))
+        model.set_splits(args.splits)
 
     roofline, kernels = None, None
     if rank == 0 and not args.no_profile:
@@ -211,6 +227,8 @@ def main():
             "path_mfma_frac": round(value * gf * 1e9 / (world * PEAK_TFLOPS * 1e12), 4),
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
         }
+        if ab:
+            line["splits_ab_img_s"] = ab
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -110,6 +110,11 @@ int miclip_zero_shot(miclip_model* m, const float* feats, int32_t B, int32_t app
                      const float* text_weights, int32_t C, float scale, float* logits,
                      int32_t* topk, int32_t k, void* stream);
 
+/* Batch split of encode_image over the caller's stream and one handle-owned
+ * stream (fork/join by events, so the call stays stream-ordered and
+ * graph-capturable): 1 = off, 2 = two halves (default, for B >= 32). */
+int miclip_set_splits(miclip_model* m, int32_t splits);
+
 void miclip_model_destroy(miclip_model* m);
 const char* miclip_last_error(void);
 int miclip_abi_version(void);
