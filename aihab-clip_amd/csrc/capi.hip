@@ -117,8 +117,8 @@ struct miclip_model {
   float* logit_scale = nullptr;
   Workspace wimg, wtxt;
   int splits = 2;               // batch split over the caller stream + aux (miclip_set_splits)
-  hipStream_t aux = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipStream_t aux[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
   // per-kernel-class HIP-event timing (miclip_set_profiling)
   struct ProfRec {
     int cls;
@@ -316,11 +316,12 @@ Workspace view(const miclip_model* m, const Workspace& w, size_t row0, size_t it
   return v;
 }
 
-int ensure_aux(miclip_model* m) {
-  if (m->aux) return 0;
-  MICLIP_HIP(hipStreamCreateWithFlags(&m->aux, hipStreamNonBlocking));
-  MICLIP_HIP(hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming));
-  MICLIP_HIP(hipEventCreateWithFlags(&m->ev_join, hipEventDisableTiming));
+int ensure_aux(miclip_model* m, int n) {
+  if (!m->ev_fork) MICLIP_HIP(hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming));
+  for (int i = 0; i < n && i < 3; ++i) {
+    if (!m->aux[i]) MICLIP_HIP(hipStreamCreateWithFlags(&m->aux[i], hipStreamNonBlocking));
+    if (!m->ev_join[i]) MICLIP_HIP(hipEventCreateWithFlags(&m->ev_join[i], hipEventDisableTiming));
+  }
   return 0;
 }
 
@@ -509,29 +510,36 @@ int miclip_encode_image(miclip_model* m, const float* images, int32_t B, float* 
   int rc;
   if ((rc = ensure_ws(m, m->wimg, B, N, W, true))) return rc;
   const int dim = (flags & MICLIP_FLAG_APPLY_PROJ) ? c.embed_dim : W;
-  // Batch split over two streams: the halves are independent images, so their
-  // kernel sequences can overlap (one half's HBM-bound epilogues / LayerNorm /
-  // attention run beside the other half's MFMA-bound GEMMs, and each GEMM's
-  // partial last wave of tiles is filled by the other stream's work).
-  const int splits = (m->splits > 1 && B >= 32 && !m->profiling) ? 2 : 1;
+  // Batch split over `splits` streams (caller's + handle-owned aux streams):
+  // the parts are independent images, so their kernel sequences overlap (one
+  // part's HBM-bound epilogues / LayerNorm / attention run beside another part's
+  // MFMA-bound GEMMs, and a GEMM's partial last wave of tiles is filled by
+  // another stream's work). Each part uses its own window of the workspace.
+  int splits = m->profiling ? 1 : m->splits;
+  while (splits > 1 && B < 16 * splits) --splits;
   if (splits == 1) return encode_image_part(m, view(m, m->wimg, 0, 0, N, W), images, B, out, flags, s);
-  if ((rc = ensure_aux(m))) return rc;
-  const int b1 = (B + 1) / 2;
+  if ((rc = ensure_aux(m, splits - 1))) return rc;
   MICLIP_HIP(hipEventRecord(m->ev_fork, s));
-  MICLIP_HIP(hipStreamWaitEvent(m->aux, m->ev_fork, 0));
-  if ((rc = encode_image_part(m, view(m, m->wimg, 0, 0, N, W), images, b1, out, flags, s)))
-    return rc;
-  if ((rc = encode_image_part(m, view(m, m->wimg, (size_t)b1 * N, b1, N, W),
-                              images + (size_t)b1 * 3 * R * R, B - b1, out + (size_t)b1 * dim,
-                              flags, m->aux)))
-    return rc;
-  MICLIP_HIP(hipEventRecord(m->ev_join, m->aux));
-  MICLIP_HIP(hipStreamWaitEvent(s, m->ev_join, 0));
+  int b0 = 0;
+  for (int p = 0; p < splits; ++p) {
+    const int nb = (B - b0) / (splits - p);
+    hipStream_t sp = p == 0 ? s : m->aux[p - 1];
+    if (p > 0) MICLIP_HIP(hipStreamWaitEvent(sp, m->ev_fork, 0));
+    if ((rc = encode_image_part(m, view(m, m->wimg, (size_t)b0 * N, b0, N, W),
+                                images + (size_t)b0 * 3 * R * R, nb, out + (size_t)b0 * dim,
+                                flags, sp)))
+      return rc;
+    b0 += nb;
+  }
+  for (int p = 1; p < splits; ++p) {
+    MICLIP_HIP(hipEventRecord(m->ev_join[p - 1], m->aux[p - 1]));
+    MICLIP_HIP(hipStreamWaitEvent(s, m->ev_join[p - 1], 0));
+  }
   return 0;
 }
 
 int miclip_set_splits(miclip_model* m, int32_t splits) {
-  if (!m || splits < 1) return fail(MICLIP_EINVAL, "splits must be >= 1");
+  if (!m || splits < 1 || splits > 4) return fail(MICLIP_EINVAL, "splits must be in [1, 4]");
   m->splits = splits;
   return 0;
 }
@@ -617,8 +625,10 @@ void miclip_model_destroy(miclip_model* m) {
   }
   for (hipEvent_t e : m->event_pool) (void)hipEventDestroy(e);
   if (m->ev_fork) (void)hipEventDestroy(m->ev_fork);
-  if (m->ev_join) (void)hipEventDestroy(m->ev_join);
-  if (m->aux) (void)hipStreamDestroy(m->aux);
+  for (int i = 0; i < 3; ++i) {
+    if (m->ev_join[i]) (void)hipEventDestroy(m->ev_join[i]);
+    if (m->aux[i]) (void)hipStreamDestroy(m->aux[i]);
+  }
   for (auto& kv : m->allocs) (void)hipFree(kv.first);
   delete m;
 }

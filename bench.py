@@ -164,7 +164,7 @@ def main():
     ab = None
     if args.ab_splits:
         ab = {}
-        for sp in (1, 2, 1, 2):
+        for sp in (1, 2, 3, 4, 2, 3, 4):
             model.set_splits(sp)
             torch.cuda.synchronize()
             t1 = time.perf_counter()

@@ -112,7 +112,8 @@ int miclip_zero_shot(miclip_model* m, const float* feats, int32_t B, int32_t app
 
 /* Batch split of encode_image over the caller's stream and one handle-owned
  * stream (fork/join by events, so the call stays stream-ordered and
- * graph-capturable): 1 = off, 2 = two halves (default, for B >= 32). */
+ * graph-capturable): 1 = off, 2..4 = that many parts (default 2; a part is
+ * never smaller than 16 images). */
 int miclip_set_splits(miclip_model* m, int32_t splits);
 
 void miclip_model_destroy(miclip_model* m);
