@@ -93,28 +93,41 @@ __global__ __launch_bounds__(1024) void attention_kernel(const T* __restrict__ q
         const i16x8 kf = *(const i16x8*)(krow + (((2 * s + hh) ^ ksw) << 4));
         sacc = Mfma<T>::m32(kf, qf[s], sacc);
       }
-      // ---- mask, online softmax (fp32, base-2) ----
-      float tmax = -INFINITY;
+      // ---- mask (only tiles that need it), online softmax in base 2 ----
+      // Scores stay raw; c2 = scale*log2(e) is folded into one FMA per element:
+      // p = exp2(s*c2 - m) with m the running max in the scaled domain.
+      const bool need_mask = (kt * 32 + 32 > N) || (CAUSAL && kt == chunk);
+      if (need_mask) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int kk = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        const bool valid = kk < N && (!CAUSAL || kk <= q);
-        sacc[r] = valid ? sacc[r] * c2 : -INFINITY;
-        tmax = fmaxf(tmax, sacc[r]);
+        for (int r = 0; r < 16; ++r) {
+          const int kk = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          const bool valid = kk < N && (!CAUSAL || kk <= q);
+          sacc[r] = valid ? sacc[r] : -INFINITY;
+        }
       }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float mnew = fmaxf(m, tmax);
-      const float alpha = exp2f(m - mnew);
-      m = mnew;
+      float tmax = fmaxf(fmaxf(sacc[0], sacc[1]), fmaxf(sacc[2], sacc[3]));
+#pragma unroll
+      for (int r = 4; r < 16; r += 4)
+        tmax = fmaxf(tmax, fmaxf(fmaxf(sacc[r], sacc[r + 1]), fmaxf(sacc[r + 2], sacc[r + 3])));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c2;
+      // Lazy rescale (cdna_hip_programming.md T13, textbook order: the decision
+      // precedes this tile's exponentials): keep the old max while the tile max
+      // exceeds it by <= 8 (p <= 2^8, exact range for fp16/bf16 P).
+      if (!__all(tmax - m <= 8.0f)) {
+        const float mnew = fmaxf(m, tmax);
+        const float alpha = exp2f(m - mnew);
+        m = mnew;
+        lsum *= alpha;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+      }
       float psum = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        sacc[r] = exp2f(sacc[r] - mnew);
+        sacc[r] = exp2f(fmaf(sacc[r], c2, -m));
         psum += sacc[r];
       }
-      lsum = lsum * alpha + psum;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+      lsum += psum;
       // ---- P^T as B operand: k-step s2 uses accumulator regs 8*s2 .. 8*s2+7 ----
       i16x8 pf[2];
 #pragma unroll
