@@ -24,11 +24,130 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <cstdlib>
+
 namespace miclip {
 
 namespace {
 
 constexpr float kLog2e = 1.4426950408889634f;
+
+// One wave: 32 queries [32*chunk, +32) of one (image, head) against all keys
+// staged in LDS (kimg / vimg). qf: this wave's Q^T fragments (B operand).
+template <typename T, bool CAUSAL>
+MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg, const i16x8 (&qf)[4], int chunk,
+                             int N, int Npad, float c2, T* op_row0, int D, int lane) {
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+  const int q = chunk * 32 + l32;
+  float m = -1e30f, lsum = 0.f;
+  f32x16 o0, o1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; }
+  const int nkt_all = Npad >> 5;
+  const int nkt = CAUSAL ? (chunk + 1 < nkt_all ? chunk + 1 : nkt_all) : nkt_all;
+  for (int kt = 0; kt < nkt; ++kt) {
+    // ---- S^T[key][q] = K . Q^T ----
+    f32x16 sacc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+    const int key = kt * 32 + l32;
+    const char* krow = kimg + key * 128;
+    const int ksw = (key >> 1) & 7;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const i16x8 kf = *(const i16x8*)(krow + (((2 * s + hh) ^ ksw) << 4));
+      sacc = Mfma<T>::m32(kf, qf[s], sacc);
+    }
+    // ---- mask (only tiles that need it), online softmax in base 2 ----
+    // Scores stay raw; c2 = scale*log2(e) is folded into one FMA per element:
+    // p = exp2(s*c2 - m) with m the running max in the scaled domain.
+    const bool need_mask = (kt * 32 + 32 > N) || (CAUSAL && kt == chunk);
+    if (need_mask) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kk = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const bool valid = kk < N && (!CAUSAL || kk <= q);
+        sacc[r] = valid ? sacc[r] : -INFINITY;
+      }
+    }
+    float tmax = fmaxf(fmaxf(sacc[0], sacc[1]), fmaxf(sacc[2], sacc[3]));
+#pragma unroll
+    for (int r = 4; r < 16; r += 4)
+      tmax = fmaxf(tmax, fmaxf(fmaxf(sacc[r], sacc[r + 1]), fmaxf(sacc[r + 2], sacc[r + 3])));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c2;
+    // Lazy rescale (cdna_hip_programming.md T13, textbook order: the decision
+    // precedes this tile's exponentials): keep the old max while the tile max
+    // exceeds it by <= 8 (p <= 2^8, exact range for fp16/bf16 P).
+    if (!__all(tmax - m <= 8.0f)) {
+      const float mnew = fmaxf(m, tmax);
+      const float alpha = exp2f(m - mnew);
+      m = mnew;
+      lsum *= alpha;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+    }
+    float psum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sacc[r] = exp2f(fmaf(sacc[r], c2, -m));
+      psum += sacc[r];
+    }
+    lsum += psum;
+    // ---- P^T as B operand: k-step s2 uses accumulator regs 8*s2 .. 8*s2+7 ----
+    i16x8 pf[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pf[s2][j] = to_bits<T>(sacc[8 * s2 + j]);
+    // ---- O^T[d][q] += V^T . P^T ----
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int kr = kt * 32 + 16 * s2 + 4 * (g >> 1) + tq;
+        const int ch = 4 * dt + 2 * (g & 1) + (tp >> 1);
+        const char* a0 = vimg + kr * 128 + ((ch ^ (tq << 1)) << 4) + 8 * (tp & 1);
+        const i16x4 lo = ds_read_tr16_b64(a0);
+        const i16x4 hi = ds_read_tr16_b64(a0 + 8 * 128);  // rows +8 keep (row & 3)
+        const i16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if (dt == 0)
+          o0 = Mfma<T>::m32(vf, pf[s2], o0);
+        else
+          o1 = Mfma<T>::m32(vf, pf[s2], o1);
+      }
+    }
+  }
+  lsum += __shfl_xor(lsum, 32, 64);
+  const float inv = 1.0f / lsum;
+  if (q < N) {
+    T* op = op_row0 + (size_t)q * D;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        i16x4 w;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          w[e] = to_bits<T>((dt == 0 ? o0[4 * rg + e] : o1[4 * rg + e]) * inv);
+        *(i16x4*)(op + 32 * dt + 8 * rg + 4 * hh) = w;
+      }
+    }
+  }
+}
+
+template <typename T>
+MICLIP_DEV void load_q(i16x8 (&qf)[4], const T* base, int ld, int chunk, int N, int lane) {
+  const int q = chunk * 32 + (lane & 31);
+  if (q < N) {
+    const T* qp = base + (size_t)q * ld + 8 * (lane >> 5);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = *(const i16x8*)(qp + 16 * s);
+  } else {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = i16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+}
 
 template <typename T, bool CAUSAL>
 __global__ __launch_bounds__(1024) void attention_kernel(const T* __restrict__ qkv,
@@ -56,133 +175,131 @@ __global__ __launch_bounds__(1024) void attention_kernel(const T* __restrict__ q
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int l32 = lane & 31, hh = lane >> 5;
-  // tr-read lane geometry: group g = lane>>4, lane 4q+p of the group
-  const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
   const float c2 = qk_scale * kLog2e;
-
   for (int chunk = wave; chunk < nchunks; chunk += nw) {
-    const int q = chunk * 32 + l32;
     i16x8 qf[4];
-    if (q < N) {
-      const T* qp = base + (size_t)q * ld + 8 * hh;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) qf[s] = *(const i16x8*)(qp + 16 * s);
-    } else {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) qf[s] = i16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    }
-
-    float m = -1e30f, lsum = 0.f;
-    f32x16 o0, o1;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; }
-
-    const int nkt_all = Npad >> 5;
-    const int nkt = CAUSAL ? (chunk + 1 < nkt_all ? chunk + 1 : nkt_all) : nkt_all;
-    for (int kt = 0; kt < nkt; ++kt) {
-      // ---- S^T[key][q] = K . Q^T ----
-      f32x16 sacc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
-      const int key = kt * 32 + l32;
-      const char* krow = kimg + key * 128;
-      const int ksw = (key >> 1) & 7;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const i16x8 kf = *(const i16x8*)(krow + (((2 * s + hh) ^ ksw) << 4));
-        sacc = Mfma<T>::m32(kf, qf[s], sacc);
-      }
-      // ---- mask (only tiles that need it), online softmax in base 2 ----
-      // Scores stay raw; c2 = scale*log2(e) is folded into one FMA per element:
-      // p = exp2(s*c2 - m) with m the running max in the scaled domain.
-      const bool need_mask = (kt * 32 + 32 > N) || (CAUSAL && kt == chunk);
-      if (need_mask) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int kk = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          const bool valid = kk < N && (!CAUSAL || kk <= q);
-          sacc[r] = valid ? sacc[r] : -INFINITY;
-        }
-      }
-      float tmax = fmaxf(fmaxf(sacc[0], sacc[1]), fmaxf(sacc[2], sacc[3]));
-#pragma unroll
-      for (int r = 4; r < 16; r += 4)
-        tmax = fmaxf(tmax, fmaxf(fmaxf(sacc[r], sacc[r + 1]), fmaxf(sacc[r + 2], sacc[r + 3])));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c2;
-      // Lazy rescale (cdna_hip_programming.md T13, textbook order: the decision
-      // precedes this tile's exponentials): keep the old max while the tile max
-      // exceeds it by <= 8 (p <= 2^8, exact range for fp16/bf16 P).
-      if (!__all(tmax - m <= 8.0f)) {
-        const float mnew = fmaxf(m, tmax);
-        const float alpha = exp2f(m - mnew);
-        m = mnew;
-        lsum *= alpha;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
-      }
-      float psum = 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        sacc[r] = exp2f(fmaf(sacc[r], c2, -m));
-        psum += sacc[r];
-      }
-      lsum += psum;
-      // ---- P^T as B operand: k-step s2 uses accumulator regs 8*s2 .. 8*s2+7 ----
-      i16x8 pf[2];
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pf[s2][j] = to_bits<T>(sacc[8 * s2 + j]);
-      // ---- O^T[d][q] += V^T . P^T ----
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          i16x4 lo, hi;
-          {
-            const int kr = kt * 32 + 16 * s2 + 4 * (g >> 1) + tq;
-            const int ch = 4 * dt + 2 * (g & 1) + (tp >> 1);
-            const char* a0 = vimg + kr * 128 + ((ch ^ (tq << 1)) << 4) + 8 * (tp & 1);
-            lo = ds_read_tr16_b64(a0);
-            hi = ds_read_tr16_b64(a0 + 8 * 128);  // rows +8 keep (row & 3)
-          }
-          const i16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          if (dt == 0)
-            o0 = Mfma<T>::m32(vf, pf[s2], o0);
-          else
-            o1 = Mfma<T>::m32(vf, pf[s2], o1);
-        }
-      }
-    }
-
-    lsum += __shfl_xor(lsum, 32, 64);
-    const float inv = 1.0f / lsum;
-    if (q < N) {
-      T* op = out + ((size_t)b * N + q) * D + h * 64;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-#pragma unroll
-        for (int rg = 0; rg < 4; ++rg) {
-          i16x4 w;
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            w[e] = to_bits<T>((dt == 0 ? o0[4 * rg + e] : o1[4 * rg + e]) * inv);
-          *(i16x4*)(op + 32 * dt + 8 * rg + 4 * hh) = w;
-        }
-      }
-    }
+    load_q<T>(qf, base, ld, chunk, N, lane);
+    attend_chunk<T, CAUSAL>(kimg, vimg, qf, chunk, N, Npad, c2,
+                            out + (size_t)b * N * D + h * 64, D, lane);
   }
 }
 
+// ---------------------------------------------------------------------------
+// Pipelined form: one 512-thread workgroup (8 waves) walks HPW consecutive
+// (image, head) pairs. The next head's K and V are staged by LDS-DMA
+// (global_load_lds_dwordx4, 1-KiB pieces of 8 rows, the K/V swizzles applied
+// to the SOURCE address) into the second LDS buffer while the current head is
+// computed, so the per-head K/V fill latency is hidden. Chunk c of head j goes
+// to wave (c + j) % 8: the short tail chunk (N = 257: one query) rotates over
+// the waves instead of always landing on the same SIMD.
+// ---------------------------------------------------------------------------
 template <typename T, bool CAUSAL>
-hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, hipStream_t s) {
+__global__ __launch_bounds__(512) void attention_pipe_kernel(const T* __restrict__ qkv,
+                                                             T* __restrict__ out, int B, int N,
+                                                             int H, int Npad, int nchunks,
+                                                             int hpw, float qk_scale) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int img_bytes = Npad * 128;            // one K or V image
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int D = H * 64, ld = 3 * D;
+  const float c2 = qk_scale * kLog2e;
+  const int bh0 = blockIdx.x * hpw;
+  const int nh = (B * H - bh0) < hpw ? (B * H - bh0) : hpw;
+  const int pieces = Npad / 8;                 // 1-KiB pieces per image
+  const int prow = lane >> 3, pch = lane & 7;
+
+  auto stage = [&](int bh, int buf) {
+    const int b = bh / H, h = bh - b * H;
+    const T* base = qkv + (size_t)b * N * ld + h * 64;
+    char* kimg = smem + buf * 2 * img_bytes;
+    char* vimg = kimg + img_bytes;
+    for (int pc = wave; pc < 2 * pieces; pc += 8) {
+      const bool isv = pc >= pieces;
+      const int piece = isv ? pc - pieces : pc;
+      const int row = piece * 8 + prow;
+      const int r = row < N ? row : N - 1;       // pad rows: finite data, masked keys
+      const int lch = isv ? (pch ^ ((row & 3) << 1)) : (pch ^ ((row >> 1) & 7));
+      glds16_hidden(base + (size_t)r * ld + (isv ? 2 * D : D) + lch * 8,
+                    (isv ? vimg : kimg) + piece * 1024);
+    }
+  };
+
+  stage(bh0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int j = 0; j < nh; ++j) {
+    const int bh = bh0 + j, b = bh / H, h = bh - b * H;
+    const T* base = qkv + (size_t)b * N * ld + h * 64;
+    const char* kimg = smem + (j & 1) * 2 * img_bytes;
+    const char* vimg = kimg + img_bytes;
+    const int c0 = ((wave - j) % 8 + 8) % 8;     // first chunk of this wave for head j
+    // Q fragments of the wave's first chunk are loaded before the next head's
+    // LDS-DMA is issued, so waiting for them never waits for that DMA.
+    i16x8 qf[4];
+    if (c0 < nchunks) load_q<T>(qf, base, ld, c0, N, lane);
+    // retire the Q loads now, naming qf as outputs so hipcc sees them defined
+    // here: otherwise it waits vmcnt(0) at the first MFMA, i.e. for the whole
+    // next-head DMA issued below (guide §5.7 item 1, form (ii)).
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])
+                 :
+                 : "memory");
+    if (j + 1 < nh) stage(bh + 1, (j + 1) & 1);
+    T* orow = out + (size_t)b * N * D + h * 64;
+    for (int c = c0; c < nchunks; c += 8) {
+      if (c != c0) {
+        load_q<T>(qf, base, ld, c, N, lane);
+        asm volatile("s_waitcnt vmcnt(0)"
+                     : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])
+                     :
+                     : "memory");
+      }
+      attend_chunk<T, CAUSAL>(kimg, vimg, qf, c, N, Npad, c2, orow, D, lane);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+}
+
+// MICLIP_ATTN=1 forces the one-head-per-workgroup kernel (A/B comparisons).
+int attn_variant() {
+  static int v = [] {
+    const char* e = getenv("MICLIP_ATTN");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+template <typename T, bool CAUSAL>
+hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, hipStream_t s,
+                       int variant) {
   const int Npad = (N + 31) & ~31;
   const int nchunks = Npad / 32;
-  const int per = (nchunks + 15) / 16;
-  const int nw = (nchunks + per - 1) / per;
   const size_t lds = (size_t)Npad * 256;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (variant == 0) variant = attn_variant();
+  // pipelined kernel: two K/V buffers must fit in LDS (N <= 320)
+  if (variant != 1 && 2 * lds <= 160 * 1024) {
+    auto kern = attention_pipe_kernel<T, CAUSAL>;
+    static bool attr_set = false;
+    if (!attr_set) {
+      const hipError_t e = hipFuncSetAttribute(
+          (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (e != hipSuccess) return e;
+      attr_set = true;
+    }
+    // enough workgroups to fill the chip twice, at most 8 heads each
+    const int heads = B * H;
+    int hpw = (heads + 511) / 512;
+    hpw = hpw < 1 ? 1 : (hpw > 8 ? 8 : hpw);
+    const int grid = (heads + hpw - 1) / hpw;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 2 * lds, s, (const T*)qkv, (T*)out, B, N, H,
+                       Npad, nchunks, hpw, 0.125f);
+    return hipGetLastError();
+  }
+  const int per = (nchunks + 15) / 16;
+  const int nw = (nchunks + per - 1) / per;
   auto kern = attention_kernel<T, CAUSAL>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -199,13 +316,13 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, hipStrea
 }  // namespace
 
 hipError_t attention(int dtype, const void* qkv, void* out, int B, int N, int H, int causal,
-                     hipStream_t s) {
+                     hipStream_t s, int variant) {
   if (B < 1 || N < 1 || H < 1) return hipErrorInvalidValue;
   if (dtype == kF16)
-    return causal ? attn_launch<_Float16, true>(qkv, out, B, N, H, s)
-                  : attn_launch<_Float16, false>(qkv, out, B, N, H, s);
-  return causal ? attn_launch<__bf16, true>(qkv, out, B, N, H, s)
-                : attn_launch<__bf16, false>(qkv, out, B, N, H, s);
+    return causal ? attn_launch<_Float16, true>(qkv, out, B, N, H, s, variant)
+                  : attn_launch<_Float16, false>(qkv, out, B, N, H, s, variant);
+  return causal ? attn_launch<__bf16, true>(qkv, out, B, N, H, s, variant)
+                : attn_launch<__bf16, false>(qkv, out, B, N, H, s, variant);
 }
 
 }  // namespace miclip

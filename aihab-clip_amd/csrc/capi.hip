@@ -664,9 +664,9 @@ int miclip_op_layernorm(int32_t dtype, const float* in, const float* gamma, cons
 }
 
 int miclip_op_attention(int32_t dtype, const void* qkv, void* out, int32_t B, int32_t N,
-                        int32_t H, int32_t causal, void* stream) {
+                        int32_t H, int32_t causal, int32_t variant, void* stream) {
   if (!qkv || !out) return fail(MICLIP_EINVAL, "null argument");
-  MICLIP_HIP(attention(dtype, qkv, out, B, N, H, causal, (hipStream_t)stream));
+  MICLIP_HIP(attention(dtype, qkv, out, B, N, H, causal, (hipStream_t)stream, variant));
   return 0;
 }
 

@@ -79,6 +79,22 @@ MICLIP_DEV void glds16(const void* g, void* lds) {
   __builtin_amdgcn_global_load_lds((const GLB_AS void*)g, (LDS_AS void*)lds, 16, 0, 0);
 }
 
+// Same DMA, issued from inline asm so hipcc's waitcnt pass does not see it:
+// hipcc then never waits vmcnt(0) for it before an unrelated ds_read or load
+// (it cannot prove the LDS ranges disjoint). The caller retires it with its
+// own `s_waitcnt vmcnt` + barrier. `lds` must be wave-uniform.
+MICLIP_DEV void glds16_hidden(const void* g, const void* lds) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane(
+      (unsigned)(size_t)(const LDS_AS void*)lds);
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g), "s"(dst)
+      : "memory");
+}
+
 MICLIP_DEV i16x4 ds_read_tr16_b64(const void* lds) {
   return __builtin_bit_cast(
       i16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4_vs*)(lds)));

@@ -77,7 +77,7 @@ def load_library(path: str = None):
         "miclip_profile_read": ([vp, ctypes.POINTER(MiclipKernelStat), i32, i32], ctypes.c_int),
         "miclip_op_gemm": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp], ctypes.c_int),
         "miclip_op_layernorm": ([i32, vp, vp, vp, vp, i32, i32, i32, vp], ctypes.c_int),
-        "miclip_op_attention": ([i32, vp, vp, i32, i32, i32, i32, vp], ctypes.c_int),
+        "miclip_op_attention": ([i32, vp, vp, i32, i32, i32, i32, i32, vp], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

@@ -81,14 +81,16 @@ def main():
         qkv = (torch.randn(M, 3 * W, device="cuda", generator=g)).to(dt)
         o = torch.empty(M, W, device="cuda", dtype=dt)
 
-        def fa():
-            rc = lib.miclip_op_attention(0, qkv.data_ptr(), o.data_ptr(), args.batch, args.tokens, H, 0, s)
-            assert rc == 0
-        ms = timeit(fa, args.iters)
-        fl = 4.0 * args.batch * H * args.tokens ** 2 * 64
-        out.append(dict(op="attention", B=args.batch, N=args.tokens, H=H, ms=round(ms, 4),
-                        tflops=round(fl / ms / 1e9, 1), gbs=round(4.0 * M * W * 2 / ms / 1e6, 1)))
-        print(json.dumps(out[-1]), flush=True)
+        for av in (1, 2, 1, 2):
+            def fa():
+                rc = lib.miclip_op_attention(0, qkv.data_ptr(), o.data_ptr(), args.batch, args.tokens, H, 0,
+                                             av, s)
+                assert rc == 0
+            ms = timeit(fa, args.iters)
+            fl = 4.0 * args.batch * H * args.tokens ** 2 * 64
+            out.append(dict(op="attention", variant=av, B=args.batch, N=args.tokens, H=H, ms=round(ms, 4),
+                            tflops=round(fl / ms / 1e9, 1), gbs=round(4.0 * M * W * 2 / ms / 1e6, 1)))
+            print(json.dumps(out[-1]), flush=True)
     if "layernorm" in args.ops:
         x = torch.randn(M, W, device="cuda", generator=g)
         gm = torch.ones(W, device="cuda")

@@ -21,7 +21,8 @@ for step in "${steps[@]}"; do
     gpu)     run gputests 1000 python -m pytest tests -m gpu -q -rf ;;
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   run bench 600 python bench.py --steps 10 --warmup 3 ;;
-    ops)     run ops 300 python scripts/bench_ops.py --variants 256,258,256,258 ;;
+    ops)     run ops 300 python scripts/bench_ops.py --variants 258 ;;
+    attn)    run attn 200 python scripts/bench_ops.py --ops attention ;;
     ksweep)  run ksweep 300 python scripts/bench_ops.py --variants 256,258 --ksweep --ops gemm ;;
     prof)    export TMPDIR=/tmp
              run prof 600 rocprofv3 --kernel-trace --stats --output-format csv \

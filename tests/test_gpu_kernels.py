@@ -109,16 +109,19 @@ def _attn_ref(qkv, B, N, H, causal):
     return o.permute(0, 2, 1, 3).reshape(B * N, H * 64)
 
 
+@pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
 @pytest.mark.parametrize("B,N,H,causal", [(2, 50, 3, 0), (3, 77, 2, 1), (2, 257, 2, 0),
                                           (1, 577, 2, 0), (2, 197, 1, 0), (1, 32, 1, 1),
-                                          (1, 1, 1, 0), (2, 100, 2, 1)])
-def test_attention(lib, dt, B, N, H, causal):
+                                          (1, 1, 1, 0), (2, 100, 2, 1), (37, 257, 16, 0),
+                                          (5, 77, 12, 1)])
+def test_attention(lib, dt, B, N, H, causal, variant):
     code, tdt = DT[dt]
     g = torch.Generator(device="cuda").manual_seed(B * 1000 + N + H + causal)
     qkv = (torch.randn(B * N, 3 * H * 64, device="cuda", generator=g) * 1.5).to(tdt)
     out = torch.empty(B * N, H * 64, device="cuda", dtype=tdt)
-    _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), out.data_ptr(), B, N, H, causal, _stream()))
+    _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), out.data_ptr(), B, N, H, causal, variant,
+                                        _stream()))
     torch.cuda.synchronize()
     ref = _attn_ref(qkv, B, N, H, causal)
     err = (out.float() - ref).abs().max().item()
@@ -133,7 +136,7 @@ def test_attention_spike(lib):
     qkv[200, 64:128] = 2.0       # key 200 in the 7th key tile -> max jumps late
     qkv = qkv.half()
     out = torch.empty(B * N, 64, device="cuda", dtype=torch.float16)
-    _check(lib, lib.miclip_op_attention(0, qkv.data_ptr(), out.data_ptr(), B, N, H, 0, _stream()))
+    _check(lib, lib.miclip_op_attention(0, qkv.data_ptr(), out.data_ptr(), B, N, H, 0, 0, _stream()))
     torch.cuda.synchronize()
     ref = _attn_ref(qkv, B, N, H, 0)
     assert (out.float() - ref).abs().max().item() < 6e-3
