@@ -95,6 +95,22 @@ MICLIP_DEV void glds16_hidden(const void* g, const void* lds) {
       : "memory");
 }
 
+// Grouped tile order: consecutive ids walk `gm` tile-rows column by column, so
+// the tiles one XCD runs together share A panels and W panels in its L2
+// (ids are already XCD-contiguous after xcd_remap). gm <= 1: row-major.
+MICLIP_DEV void group_tile(int id, int ntm, int ntn, int gm, int& tm, int& tn) {
+  if (gm <= 1) {
+    tm = id / ntn;
+    tn = id - tm * ntn;
+    return;
+  }
+  const int per = gm * ntn, g = id / per, first = g * gm;
+  const int rows = ntm - first < gm ? ntm - first : gm;
+  const int idx = id - g * per;
+  tm = first + idx % rows;
+  tn = idx / rows;
+}
+
 MICLIP_DEV i16x4 ds_read_tr16_b64(const void* lds) {
   return __builtin_bit_cast(
       i16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4_vs*)(lds)));

@@ -268,7 +268,7 @@ MICLIP_DEV void lds_barrier() {
 template <typename T, class Epi, int SCHED>
 __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
                                                       const T* __restrict__ W, int M, int N,
-                                                      int K, Epi epi) {
+                                                      int K, Epi epi, int gm) {
   constexpr int HALF = 128 * 128;  // bytes of one half-tile slot
   constexpr int EPI_LD = 260;      // fp32 row stride of the epilogue staging (pad 4)
   constexpr int SMEM = 128 * EPI_LD * 4 > 8 * HALF ? 128 * EPI_LD * 4 : 8 * HALF;
@@ -278,8 +278,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int ntn = N / 256, ntm = (M + 255) / 256;
-  const int bid = xcd_remap(blockIdx.x, ntm * ntn);
-  const int tm = bid / ntn, tn = bid - tm * ntn;
+  int tm, tn;
+  group_tile(xcd_remap(blockIdx.x, ntm * ntn), ntm, ntn, gm, tm, tn);
   const int m0 = tm * 256, n0 = tn * 256;
 
   // LDS-DMA sources: slot row sr = piece*8 + (lane>>3), piece = wave*2 + pp
@@ -878,6 +878,18 @@ int gemm_variant() {
   return v;
 }
 
+// Tile-row group of the 256x256 kernel's grouped order (MICLIP_GEMM_GROUP,
+// default 4; 1 = plain row-major). A variant >= 1000 carries it in its
+// thousands digit (diagnostic A/B through miclip_op_gemm).
+int gemm_group() {
+  static int g = [] {
+    const char* e = getenv("MICLIP_GEMM_GROUP");
+    const int v = e ? atoi(e) : 4;
+    return v < 1 ? 1 : v;
+  }();
+  return g;
+}
+
 bool gemm_shape_ok(int M, int N, int K) {
   return M >= 1 && N >= 128 && K >= BK && N % 128 == 0 && K % BK == 0;
 }
@@ -886,6 +898,8 @@ template <typename T, class Epi>
 hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hipStream_t s,
                   int variant = 0) {
   if (!gemm_shape_ok(M, N, K)) return hipErrorInvalidValue;
+  const int gm = variant >= 1000 ? variant / 1000 : gemm_group();
+  variant %= 1000;
   if (variant == 0) variant = gemm_variant();
   if (variant != 0 && variant != 128 && variant != 256 && variant != 257 && variant != 258 &&
       variant != 2 && variant != 3)
@@ -919,13 +933,13 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
     // default: the staggered schedule (SCHED 2); 256 / 257 select SCHED 0 / 1
     if (variant == 257)
       hipLaunchKernelGGL((gemm256_kernel<T, Epi, 1>), dim3(tiles256), dim3(512), 0, s,
-                         (const T*)A, (const T*)W, M, N, K, epi);
+                         (const T*)A, (const T*)W, M, N, K, epi, gm);
     else if (variant == 256)
       hipLaunchKernelGGL((gemm256_kernel<T, Epi, 0>), dim3(tiles256), dim3(512), 0, s,
-                         (const T*)A, (const T*)W, M, N, K, epi);
+                         (const T*)A, (const T*)W, M, N, K, epi, gm);
     else
       hipLaunchKernelGGL((gemm256_kernel<T, Epi, 2>), dim3(tiles256), dim3(512), 0, s,
-                         (const T*)A, (const T*)W, M, N, K, epi);
+                         (const T*)A, (const T*)W, M, N, K, epi, gm);
     return hipGetLastError();
   }
   constexpr int BM = 128, BN = 128;

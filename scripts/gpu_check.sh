@@ -23,6 +23,8 @@ for step in "${steps[@]}"; do
     bench)   run bench 600 python bench.py --steps 10 --warmup 3 ;;
     ops)     run ops 300 python scripts/bench_ops.py --variants 258 ;;
     attn)    run attn 200 python scripts/bench_ops.py --ops attention ;;
+    group)   run group 300 python scripts/bench_ops.py --ops gemm --variants 1258,4258,8258,2258,1258,4258 ;;
+    traffic) run traffic 700 bash scripts/pmc.sh traffic ;;
     ksweep)  run ksweep 300 python scripts/bench_ops.py --variants 256,258 --ksweep --ops gemm ;;
     prof)    export TMPDIR=/tmp
              run prof 600 rocprofv3 --kernel-trace --stats --output-format csv \

@@ -1,20 +1,35 @@
 #!/bin/bash
 # PMC counter passes (one rocprofv3 run per counter group, kernel-trace only, no
-# other tracing) over the GEMM micro-benchmark. Output: gpurun_out/pmc/<pass>/
+# other tracing). Output: gpurun_out/pmc/<pass>/
+#   pmc.sh            -> occupancy / MFMA / LDS / L2 groups over the fc+proj GEMMs
+#   pmc.sh traffic    -> FETCH_SIZE and WRITE_SIZE over gemm_fc, then scripts/traffic.py
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc
-CMD=(python3 scripts/bench_ops.py --ops gemm --only fc,proj --variants 256,257 --iters 5)
+pass() {
+  local name=$1; shift
+  local ctrs=$1; shift
+  echo "=== pass $name: $ctrs"
+  timeout -k 10 300 rocprofv3 --pmc $ctrs --kernel-trace --output-format csv \
+      -d "$PWD/gpurun_out/pmc/$name" -o run -- "$@" > "gpurun_out/pmc/$name.log" 2>&1
+  local rc=$?
+  echo "pass $name rc=$rc"; tail -3 "gpurun_out/pmc/$name.log"
+  if [ $rc -ne 0 ]; then echo "stopping"; exit $rc; fi
+}
+if [ "${1:-}" = traffic ]; then
+  CMD=(python3 scripts/bench_ops.py --ops gemm --only fc --variants 0 --iters 5)
+  pass fetch FETCH_SIZE "${CMD[@]}"
+  pass write WRITE_SIZE "${CMD[@]}"
+  python3 scripts/traffic.py
+  exit $?
+fi
+CMD=(python3 scripts/bench_ops.py --ops gemm --only fc,proj --variants 0 --iters 5)
 i=0
 for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
            "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_LDS SQ_WAIT_INST_LDS" \
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL" \
            "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  echo "=== pass $i: $grp"
-  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$PWD/gpurun_out/pmc/p$i" -o run -- "${CMD[@]}" > gpurun_out/pmc/p$i.log 2>&1
-  rc=$?
-  echo "pass $i rc=$rc"; tail -3 gpurun_out/pmc/p$i.log
-  if [ $rc -ne 0 ]; then echo "stopping"; exit $rc; fi
+  pass "p$i" "$grp" "${CMD[@]}"
 done

@@ -1,0 +1,55 @@
+#!/usr/bin/env python
+"""HBM-side bytes per launch of the MLP c_fc GEMM from two rocprofv3 PMC passes.
+
+Reads gpurun_out/pmc/{fetch,write}/run_counter_collection.csv written by
+`scripts/pmc.sh traffic` (bench_ops.py --only fc: M=65792 N=4096 K=1024, the
+bench's gemm_fc launch) and writes profiles/traffic_gemm_fc.json, which
+bench.py reports as roofline.traffic.
+
+Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are
+KiB; on gfx950 FETCH_SIZE tallies 128-B streaming reads at 64 B, so it is
+doubled; WRITE_SIZE is exact for 16-B/lane stores. Both count L2 memory-side
+requests, i.e. Infinity-Cache hits are included (an upper bound on HBM bytes).
+"""
+import csv
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+M, N, K = 65792, 4096, 1024
+
+
+def launches(path, counter):
+    vals = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if (r["Counter_Name"] == counter and "gemm256_kernel" in r["Kernel_Name"]
+                    and "EpiStore" in r["Kernel_Name"]
+                    and int(r["Grid_Size"]) == ((M + 255) // 256) * (N // 256) * 512):
+                vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    d = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "pmc")
+    fetch = launches(os.path.join(d, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = launches(os.path.join(d, "write", "run_counter_collection.csv"), "WRITE_SIZE")
+    if not fetch or not write:
+        sys.exit("no gemm_fc launches found in the PMC passes")
+    rd = 2.0 * 1024 * statistics.median(fetch)
+    wr = 1024 * statistics.median(write)
+    algo = 2 * M * K + 2 * N * K + 2 * M * N
+    out = {"kernel": "gemm_fc", "model": "ViT-L/14", "batch": 256, "M": M, "N": N, "K": K,
+           "hbm_bytes_per_launch": round(rd + wr), "read_bytes": round(rd), "write_bytes": round(wr),
+           "algorithmic_bytes": algo, "launches": [len(fetch), len(write)],
+           "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), KiB x1024, "
+                     "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B); median over launches"}
+    with open(os.path.join(ROOT, "profiles", "traffic_gemm_fc.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
