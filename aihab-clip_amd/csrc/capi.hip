@@ -133,6 +133,8 @@ struct miclip_model {
     double ms = 0, flops = 0, bytes = 0;
   };
   std::vector<ProfAcc> prof_acc;
+  miclip_image_desc* pre_desc = nullptr;   // device copy of miclip_preprocess descriptors
+  int pre_cap = 0;
 };
 
 namespace {
@@ -580,6 +582,34 @@ int miclip_zero_shot(miclip_model* m, const float* feats, int32_t B, int32_t app
   const int Din = apply_proj ? m->cfg.vision_width : E;
   MICLIP_HIP(zero_shot(feats, apply_proj ? m->vproj : nullptr, text_weights, logits,
                        topk, B, Din, E, C, scale, topk ? k : 0, (hipStream_t)stream));
+  return 0;
+}
+
+int miclip_preprocess(miclip_model* m, const uint8_t* pixels, const miclip_image_desc* descs,
+                      int32_t B, void* out, int32_t out_kind, void* stream) {
+  if (!m || !pixels || !descs || !out || B < 1)
+    return fail(MICLIP_EINVAL, "bad argument to preprocess");
+  const hipStream_t s = (hipStream_t)stream;
+  if (B > m->pre_cap) {
+    if (m->pre_desc) {
+      MICLIP_HIP(hipStreamSynchronize(s));   // the old buffer may still be read
+      dev_free(m, m->pre_desc);
+      m->pre_desc = nullptr;
+      m->pre_cap = 0;
+    }
+    const int cap = B < 256 ? 256 : B;
+    if (int rc = dev_alloc(m, (void**)&m->pre_desc, sizeof(miclip_image_desc) * cap)) return rc;
+    m->pre_cap = cap;
+  }
+  char err[256] = {0};
+  // pageable source: the copy has consumed `descs` when hipMemcpyAsync returns
+  MICLIP_HIP(hipMemcpyAsync(m->pre_desc, descs, sizeof(miclip_image_desc) * B,
+                            hipMemcpyHostToDevice, s));
+  const hipError_t e = preprocess(pixels, descs, m->pre_desc, B, m->cfg.image_resolution,
+                                  out_kind, out, s, err, sizeof(err));
+  if (e != hipSuccess)
+    return fail(e == hipErrorInvalidValue ? MICLIP_EINVAL : MICLIP_EHIP,
+                err[0] ? std::string(err) : std::string("preprocess: ") + hipGetErrorString(e));
   return 0;
 }
 

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "miclip.h"
+
 namespace miclip {
 
 enum Act { ACT_NONE = 0, ACT_QUICKGELU = 1, ACT_GELU = 2 };
@@ -67,5 +69,13 @@ hipError_t row_l2norm(float* x, int R, int D, hipStream_t s);
 hipError_t zero_shot(const float* x, const float* proj, const float* tw, float* logits,
                      int32_t* topk, int B, int Din, int E, int C, float scale, int k,
                      hipStream_t s);
+
+// ---- on-device CLIP preprocessing (bicubic resize + center crop + normalise) ----
+// descs_host / descs_dev: the same B descriptors on host (validated, sizes the
+// launch) and in device memory (read by the kernel); out_kind 0 = float32
+// [B,3,n,n] normalised, 1 = uint8 [B,n,n,3]. On error fills `err`.
+hipError_t preprocess(const uint8_t* pixels, const miclip_image_desc* descs_host,
+                      const miclip_image_desc* descs_dev, int B, int n, int out_kind, void* out,
+                      hipStream_t s, char* err, int errlen);
 
 }  // namespace miclip

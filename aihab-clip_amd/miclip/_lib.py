@@ -22,8 +22,11 @@ EXPORTS = (
     "miclip_encode_image", "miclip_encode_text", "miclip_zero_shot",
     "miclip_model_destroy", "miclip_last_error", "miclip_abi_version",
     "miclip_model_bytes", "miclip_set_profiling", "miclip_profile_read", "miclip_set_splits",
-    "miclip_op_gemm", "miclip_op_layernorm", "miclip_op_attention",
+    "miclip_op_gemm", "miclip_op_layernorm", "miclip_op_attention", "miclip_preprocess",
 )
+
+MICLIP_PRE_F32 = 0
+MICLIP_PRE_U8 = 1
 
 
 class MiclipConfig(ctypes.Structure):
@@ -40,6 +43,11 @@ class MiclipTensor(ctypes.Structure):
 class MiclipKernelStat(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char_p), ("launches", ctypes.c_int64), ("ms", ctypes.c_double),
                 ("flops", ctypes.c_double), ("bytes", ctypes.c_double)]
+
+
+class MiclipImageDesc(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_int64), ("height", ctypes.c_int32), ("width", ctypes.c_int32),
+                ("channels", ctypes.c_int32), ("row_stride", ctypes.c_int32)]
 
 
 class MiclipError(RuntimeError):
@@ -78,6 +86,8 @@ def load_library(path: str = None):
         "miclip_op_gemm": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp], ctypes.c_int),
         "miclip_op_layernorm": ([i32, vp, vp, vp, vp, i32, i32, i32, vp], ctypes.c_int),
         "miclip_op_attention": ([i32, vp, vp, i32, i32, i32, i32, i32, vp], ctypes.c_int),
+        "miclip_preprocess": ([vp, vp, ctypes.POINTER(MiclipImageDesc), i32, vp, i32, vp],
+                              ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

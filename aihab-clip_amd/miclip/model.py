@@ -213,6 +213,61 @@ class CLIP(nn.Module):
         return out
 
     @torch.no_grad()
+    def preprocess_images(self, images, uint8=False, out=None):
+        """On-device `_transform(R)` (clip/clip.py:74-81) of decoded uint8 images.
+
+        images: a uint8 tensor [B, H, W, C] (any device) or a list of uint8
+        HxWxC / HxW arrays or tensors (sizes may differ); C is 3 (RGB) or 1 (L).
+        Returns float32 [B, 3, R, R] (ToTensor + Normalize), or with uint8=True
+        the resized + center-cropped pixels uint8 [B, R, R, 3]; bit-exact with
+        Pillow's bicubic resize + torchvision's crop.
+        """
+        h = self._require()
+        R = self.config.image_resolution
+        if isinstance(images, torch.Tensor) and images.dim() == 4:
+            if images.dtype != torch.uint8:
+                raise ValueError("images must be uint8")
+            buf = images.to(self.device).contiguous()
+            B, H, W, C = buf.shape
+            descs = (_lib.MiclipImageDesc * max(B, 1))(
+                *[_lib.MiclipImageDesc(i * H * W * C, H, W, C, 0) for i in range(B)])
+        else:
+            arrs = []
+            for im in images:
+                a = im.cpu().numpy() if isinstance(im, torch.Tensor) else np.asarray(im)
+                if a.dtype != np.uint8:
+                    raise ValueError("images must be uint8")
+                if a.ndim == 2:
+                    a = a[:, :, None]
+                if a.ndim != 3:
+                    raise ValueError(f"expected HxWxC images, got shape {a.shape}")
+                arrs.append(np.ascontiguousarray(a))
+            B = len(arrs)
+            offs = np.cumsum([0] + [a.size for a in arrs])
+            host = torch.from_numpy(np.concatenate([a.reshape(-1) for a in arrs])) if B else \
+                torch.empty(0, dtype=torch.uint8)
+            buf = host.pin_memory().to(self.device, non_blocking=True) if B else host
+            descs = (_lib.MiclipImageDesc * max(B, 1))(
+                *[_lib.MiclipImageDesc(int(offs[i]), a.shape[0], a.shape[1], a.shape[2], 0)
+                  for i, a in enumerate(arrs)])
+        shape = (B, R, R, 3) if uint8 else (B, 3, R, R)
+        dt = torch.uint8 if uint8 else torch.float32
+        if out is None:
+            out = torch.empty(shape, device=self.device, dtype=dt)
+        elif tuple(out.shape) != shape or out.dtype != dt or not out.is_contiguous():
+            raise ValueError(f"out must be a contiguous {dt} tensor of shape {shape}")
+        if B == 0:
+            return out
+        with torch.cuda.device(self.device):
+            _lib.check(h.lib.miclip_preprocess(h.ptr, buf.data_ptr(), descs, B, out.data_ptr(),
+                                               _lib.MICLIP_PRE_U8 if uint8 else _lib.MICLIP_PRE_F32,
+                                               _lib.stream_handle(self.device)),
+                       "miclip_preprocess")
+        if buf.is_cuda:
+            buf.record_stream(torch.cuda.current_stream(self.device))
+        return out
+
+    @torch.no_grad()
     def encode_text(self, text):
         """(x_before_proj [P, transformer_width], x [P, embed_dim]) (clip/model.py:338-353)."""
         h = self._require()

@@ -2,8 +2,9 @@
 
 clip/clip.py:74-81: Resize(n_px, BICUBIC) on the shorter side -> CenterCrop(n_px)
 -> RGB -> ToTensor -> Normalize(CLIP_MEAN, CLIP_STD). torchvision is not in the
-image, so this restates it on PIL + numpy. It is host preprocessing (SURVEY §8f
-row 1 is the on-device version, out of this round's scope).
+image, so this restates it on PIL + numpy. This is the host path;
+`CLIP.preprocess_images` is the on-device kernel with
+bit-identical output.
 """
 import numpy as np
 import torch
@@ -20,8 +21,11 @@ class Transform:
         if isinstance(image, np.ndarray):
             image = Image.fromarray(image)
         w, h = image.size
-        s = self.n_px / min(w, h)
-        nw, nh = max(self.n_px, round(w * s)), max(self.n_px, round(h * s))
+        # torchvision Resize(int): short side -> n, long side -> int(n * long / short)
+        if w <= h:
+            nw, nh = self.n_px, int(self.n_px * h / w)
+        else:
+            nw, nh = int(self.n_px * w / h), self.n_px
         image = image.resize((nw, nh), Image.BICUBIC)
         left = int(round((nw - self.n_px) / 2.0))
         top = int(round((nh - self.n_px) / 2.0))

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MICLIP_ABI_VERSION 1
+#define MICLIP_ABI_VERSION 2
 
 enum miclip_status {
   MICLIP_OK = 0,
@@ -109,6 +109,32 @@ int miclip_encode_text(miclip_model* m, const int64_t* tokens, int32_t P, float*
 int miclip_zero_shot(miclip_model* m, const float* feats, int32_t B, int32_t apply_proj,
                      const float* text_weights, int32_t C, float scale, float* logits,
                      int32_t* topk, int32_t k, void* stream);
+
+/* One decoded image in device memory: interleaved HWC uint8 ('RGB' or 'L'). */
+typedef struct miclip_image_desc {
+  int64_t offset;     /* byte offset of pixel (0, 0) from the `pixels` base */
+  int32_t height;
+  int32_t width;
+  int32_t channels;   /* 3 (RGB) or 1 (L; replicated to RGB like convert("RGB")) */
+  int32_t row_stride; /* bytes between rows; 0 = width * channels */
+} miclip_image_desc;
+
+enum miclip_pre_out {
+  MICLIP_PRE_F32 = 0, /* float32 [B, 3, R, R], ToTensor + Normalize(CLIP_MEAN, CLIP_STD) */
+  MICLIP_PRE_U8 = 1   /* uint8 [B, R, R, 3], the resized + center-cropped RGB pixels */
+};
+
+/* On-device CLIP preprocessing, R = the model's image_resolution. Replaces the
+ * per-image CPU transform of clip/clip.py:74-81 (`_transform`) and
+ * data/clip_transforms.py:50-55 (test split): Resize(R, BICUBIC) of the shorter
+ * side -> CenterCrop(R) -> RGB -> ToTensor -> Normalize; bit-exact with
+ * Pillow's resize (libImaging/Resample.c) and torchvision's size/anchor rules.
+ * pixels: device uint8 base; descs: HOST array [B] (copied, stream-ordered,
+ * into a handle-owned device buffer before return); out: device, see
+ * miclip_pre_out. Images may differ in size (ragged batch). Errors: EINVAL for
+ * a bad descriptor or a downscale beyond 64 taps (about 16x at R = 224). */
+int miclip_preprocess(miclip_model* m, const uint8_t* pixels, const miclip_image_desc* descs,
+                      int32_t B, void* out, int32_t out_kind, void* stream);
 
 /* Batch split of encode_image over the caller's stream and one handle-owned
  * stream (fork/join by events, so the call stays stream-ordered and

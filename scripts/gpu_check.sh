@@ -22,6 +22,7 @@ for step in "${steps[@]}"; do
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   run bench 600 python bench.py --steps 10 --warmup 3 ;;
     ops)     run ops 300 python scripts/bench_ops.py --variants 258 ;;
+    pre)     run pre 300 python -m pytest tests/test_preprocess.py -q -rf ;;
     attn)    run attn 200 python scripts/bench_ops.py --ops attention ;;
     group)   run group 300 python scripts/bench_ops.py --ops gemm --variants 1258,4258,8258,2258,1258,4258 ;;
     traffic) run traffic 700 bash scripts/pmc.sh traffic ;;
