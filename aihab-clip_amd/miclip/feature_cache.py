@@ -8,7 +8,13 @@ Counterparts (same names, arguments, outputs, file layout and error behaviour):
   * _feature_cache_dir / _embedding_cache_dir / _canonical_backbone_name /
     _feature_cache_exists          aihab_utils/feature_cache.py:18-65, 253-261
 
-plus the multi-GPU variant the reference does not have:
+plus what the reference does not have:
+  * AsyncHostSink: in-order asynchronous D2H of each batch into pinned host
+    memory on a side stream instead of a synchronous
+    `.to("cpu")` per batch;
+  * prepare_images: loaders may yield decoded uint8 images, transformed on
+    the GPU by `CLIP.preprocess_images` (SURVEY §8f row 1);
+and the multi-GPU variant:
   * shard_range / sharded_encode / compute_image_features_sharded: each rank
     encodes a contiguous slice of the image batch and the L2-normalised (or
     raw) embeddings are all-gathered over RCCL (torch.distributed backend
@@ -82,21 +88,89 @@ def _model_device(clip_model):
         return torch.device("cuda")
 
 
+class AsyncHostSink:
+    """In-order device -> host copies that never stall the encode loop.
+
+    The reference moves every batch to the host with a synchronous
+    `.to("cpu")` (methods/utils.py:164, aihab_utils/feature_cache.py:131),
+    which drains the GPU once per batch. Here each pushed device tensor is
+    copied on a side HIP stream (ordered after the producing stream by a
+    stream wait) into pinned host memory; at most `depth` copies are in flight
+    (older ones are waited for, so device memory held by pending copies stays
+    bounded). `result()` waits for the tail and concatenates in push order.
+    CPU tensors pass straight through.
+    """
+
+    def __init__(self, depth: int = 4):
+        self.depth = max(1, int(depth))
+        self._pending = []
+        self._parts = []
+        self._stream = None
+
+    def push(self, t: torch.Tensor) -> None:
+        t = t.detach()
+        if not t.is_cuda:
+            self._parts.append(t)
+            return
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(t.device)
+        cur = torch.cuda.current_stream(t.device)
+        self._stream.wait_stream(cur)
+        host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        with torch.cuda.stream(self._stream):
+            host.copy_(t, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self._stream)
+        t.record_stream(self._stream)
+        self._pending.append(ev)
+        self._parts.append(host)
+        while len(self._pending) > self.depth:
+            self._pending.pop(0).synchronize()
+
+    def result(self) -> torch.Tensor:
+        for ev in self._pending:
+            ev.synchronize()
+        self._pending.clear()
+        return torch.cat(self._parts, dim=0) if self._parts else torch.empty(0)
+
+
+def is_raw_batch(images) -> bool:
+    """True for decoded uint8 images (list of HxWxC arrays/tensors or a uint8 [B,H,W,C])."""
+    if isinstance(images, torch.Tensor):
+        return images.dtype == torch.uint8 and images.dim() == 4
+    return isinstance(images, (list, tuple)) and len(images) > 0 and \
+        getattr(images[0], "dtype", None) in (np.uint8, torch.uint8)
+
+
+def prepare_images(model, images, device):
+    """Model-ready float32 [B,3,R,R] on `device`: decoded uint8 batches go through the
+    on-device transform (`CLIP.preprocess_images`); tensors that
+    the loader already transformed (the reference's path) are moved as they are."""
+    if is_raw_batch(images):
+        if not hasattr(model, "preprocess_images"):
+            raise ValueError("uint8 image batches need a miclip model (on-device preprocessing)")
+        return model.preprocess_images(images)
+    return images.to(device, non_blocking=True)
+
+
 @torch.no_grad()
 def compute_image_features(clip_model, loader, to_cpu: bool = False):
-    """Pre-projection features and labels of every batch (methods/utils.py:142-173)."""
+    """Pre-projection features and labels of every batch (methods/utils.py:142-173).
+
+    With to_cpu the per-batch host copies are asynchronous (AsyncHostSink);
+    loaders may also yield decoded uint8 images (prepare_images)."""
     device = _model_device(clip_model)
-    feats, labels = [], []
+    feats, labels = ([], []) if not to_cpu else (AsyncHostSink(), [])
     for images, target in loader:
-        images = images.to(device, non_blocking=True)
-        x = clip_model.encode_image(images)
+        x = clip_model.encode_image(prepare_images(clip_model, images, device))
         if to_cpu:
-            feats.append(x.detach().to("cpu"))
+            feats.push(x)
             labels.append(target.detach().to("cpu"))
         else:
             feats.append(x)
             labels.append(target.to(device, non_blocking=True))
-    return torch.cat(feats, dim=0), torch.cat(labels, dim=0)
+    feats = feats.result() if to_cpu else torch.cat(feats, dim=0)
+    return feats, torch.cat(labels, dim=0)
 
 
 @torch.no_grad()
@@ -144,7 +218,7 @@ def cache_openclip_embeddings(cfg: dict, model, loader, split: str = "test",
     cache_dir.mkdir(parents=True, exist_ok=True)
     device = _model_device(model)
     model.eval()
-    feats_list, labels_list, rows = [], [], []
+    sink, labels_list, rows = AsyncHostSink(), [], []
     for batch in loader:
         if isinstance(batch, (list, tuple)) and len(batch) == 3:
             images, targets, metadata = batch
@@ -153,14 +227,14 @@ def cache_openclip_embeddings(cfg: dict, model, loader, split: str = "test",
             metadata = None
         else:
             raise ValueError("Expected batch to be (images, targets) or (images, targets, metadata).")
-        images = images.to(device, non_blocking=True)
+        images = prepare_images(model, images, device)
         if hasattr(model, "zero_shot"):          # miclip model: normalise fused into ln_post
             feats = model.encode_image(images, normalize=normalize)
         else:
             feats = model.encode_image(images)
             if normalize:
                 feats = F.normalize(feats, dim=-1)
-        feats_list.append(feats.detach().to("cpu"))
+        sink.push(feats)
         t = targets.detach().to("cpu")
         labels_list.append(t)
         for i, row in enumerate(_metadata_rows(metadata, int(t.shape[0]))):
@@ -168,7 +242,7 @@ def cache_openclip_embeddings(cfg: dict, model, loader, split: str = "test",
                          "ground_truth_num_label": int(t[i].item()),
                          "ground_truth_word_label": row.get("plot_word_label", ""),
                          "ground_truth_L2_num_label": row.get("l2_label", -1)})
-    feats_all = torch.cat(feats_list, dim=0)
+    feats_all = sink.result()
     labels_all = torch.cat(labels_list, dim=0)
     torch.save(feats_all, cache_dir / "embeddings.pt")
     torch.save(labels_all, cache_dir / "labels.pt")
@@ -228,14 +302,20 @@ def sharded_encode(encode_fn, images: torch.Tensor, group=None, dim: Optional[in
         return encode_fn(images)
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    n = images.shape[0]
+    n = images.shape[0] if isinstance(images, torch.Tensor) else len(images)
     lo, hi = shard_range(n, rank, world)
     local = encode_fn(images[lo:hi]) if hi > lo else None
     width = dim if dim is not None else (local.shape[1] if local is not None else None)
     if width is None:
         raise ValueError("sharded_encode needs `dim` when a rank has an empty shard")
     per = -(-n // world)
-    dev = local.device if local is not None else images.device
+    if local is not None:
+        dev = local.device
+    elif isinstance(images, torch.Tensor):
+        dev = images.device
+    else:
+        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
+            else torch.device("cpu")
     buf = torch.zeros(per, width, device=dev, dtype=torch.float32)
     if local is not None:
         buf[: hi - lo] = local
@@ -256,7 +336,7 @@ def compute_image_features_sharded(clip_model, loader, normalize: bool = True, g
     dim = clip_model.config.vision_width
 
     def enc(x):
-        return clip_model.encode_image(x.to(device, non_blocking=True), normalize=normalize)
+        return clip_model.encode_image(prepare_images(clip_model, x, device), normalize=normalize)
     feats, labels = [], []
     for images, target in loader:
         feats.append(sharded_encode(enc, images, group=group, dim=dim))
