@@ -279,8 +279,12 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, hipStrea
   const size_t lds = (size_t)Npad * 256;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (variant == 0) variant = attn_variant();
-  // pipelined kernel: two K/V buffers must fit in LDS (N <= 320)
-  if (variant != 1 && 2 * lds <= 160 * 1024) {
+  // pipelined kernel (opt-in, variant 2): two K/V buffers must fit in LDS
+  // (N <= 320). Measured slower at N = 257 (0.27 vs 0.24-0.26 ms per ViT-L
+  // layer): 9 query chunks on 8 waves leave one wave with two chunks before
+  // every per-head barrier, and 2 one-head workgroups per CU already overlap
+  // one head's K/V load with the other's compute.
+  if (variant == 2 && 2 * lds <= 160 * 1024) {
     auto kern = attention_pipe_kernel<T, CAUSAL>;
     static bool attr_set = false;
     if (!attr_set) {

@@ -42,8 +42,8 @@ hipError_t layernorm(int dtype, const float* in, const int32_t* rows, int in_str
 // ---- fused multi-head attention over a packed QKV buffer ----
 // qkv: [B*N, 3*H*64] compute dtype (torch in_proj order q|k|v); out: [B*N, H*64].
 // head dim 64; causal adds the -inf strictly-upper-triangular mask (clip/model.py:323-329).
-// variant: 0 = pick (pipelined multi-head kernel when two K/V buffers fit),
-// 1 = one head per workgroup, 2 = force pipelined.
+// variant: 0 = default (MICLIP_ATTN env, else one head per workgroup),
+// 1 = one head per workgroup, 2 = pipelined multi-head kernel (N <= 320).
 hipError_t attention(int dtype, const void* qkv, void* out, int B, int N, int H, int causal,
                      hipStream_t s, int variant = 0);
 

@@ -68,9 +68,9 @@ def _tiny_model(n):
     import miclip
     from miclip.configs import CLIPConfig
     from miclip.weights import generate_state_dict
-    cfg = CLIPConfig(embed_dim=64, image_resolution=n, vision_layers=1, vision_width=128,
+    cfg = CLIPConfig(embed_dim=64, image_resolution=n, vision_layers=1, vision_width=256,
                      vision_patch_size=n // 7, context_length=77, vocab_size=49408,
-                     transformer_width=128, transformer_heads=2, transformer_layers=1)
+                     transformer_width=256, transformer_heads=4, transformer_layers=1)
     sd = {k: torch.from_numpy(v) for k, v in generate_state_dict(cfg, seed=0).items()}
     return miclip.CLIP(cfg, sd, device="cuda")
 
