@@ -185,23 +185,27 @@ __global__ __launch_bounds__(1024) void attention_kernel(const T* __restrict__ q
 }
 
 // ---------------------------------------------------------------------------
-// Pipelined form: one 512-thread workgroup (8 waves) walks HPW consecutive
-// (image, head) pairs. The next head's K and V are staged by LDS-DMA
-// (global_load_lds_dwordx4, 1-KiB pieces of 8 rows, the K/V swizzles applied
-// to the SOURCE address) into the second LDS buffer while the current head is
-// computed, so the per-head K/V fill latency is hidden. Chunk c of head j goes
-// to wave (c + j) % 8: the short tail chunk (N = 257: one query) rotates over
-// the waves instead of always landing on the same SIMD.
+// Pipelined form: one workgroup of nchunks waves (wave w owns query chunk w,
+// N <= 320 -> at most 10 waves) walks hpw consecutive (image, head) pairs.
+// While head j is computed, head j+1's K and V are LDS-DMA'd
+// (global_load_lds_dwordx4 issued from inline asm, 1-KiB pieces of 8 rows,
+// the K/V swizzles applied to the SOURCE address) into the other LDS buffer
+// and each wave's Q fragments for head j+1 are loaded into registers, so the
+// K/V/Q fetch of the next head runs under this head's MFMA + softmax work.
+// One barrier per head: at its top every wave has retired its own DMA and Q
+// loads (s_waitcnt vmcnt(0)) and finished reading the buffer that the next
+// DMA overwrites.
 // ---------------------------------------------------------------------------
 template <typename T, bool CAUSAL>
-__global__ __launch_bounds__(512) void attention_pipe_kernel(const T* __restrict__ qkv,
+__global__ __launch_bounds__(640) void attention_pipe_kernel(const T* __restrict__ qkv,
                                                              T* __restrict__ out, int B, int N,
-                                                             int H, int Npad, int nchunks,
-                                                             int hpw, float qk_scale) {
+                                                             int H, int Npad, int hpw,
+                                                             float qk_scale) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int img_bytes = Npad * 128;            // one K or V image
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nw = blockDim.x >> 6;              // == nchunks
   const int D = H * 64, ld = 3 * D;
   const float c2 = qk_scale * kLog2e;
   const int bh0 = blockIdx.x * hpw;
@@ -209,12 +213,15 @@ __global__ __launch_bounds__(512) void attention_pipe_kernel(const T* __restrict
   const int pieces = Npad / 8;                 // 1-KiB pieces per image
   const int prow = lane >> 3, pch = lane & 7;
 
-  auto stage = [&](int bh, int buf) {
+  auto head_base = [&](int bh) {
     const int b = bh / H, h = bh - b * H;
-    const T* base = qkv + (size_t)b * N * ld + h * 64;
+    return qkv + (size_t)b * N * ld + h * 64;
+  };
+  auto stage = [&](int bh, int buf) {
+    const T* base = head_base(bh);
     char* kimg = smem + buf * 2 * img_bytes;
     char* vimg = kimg + img_bytes;
-    for (int pc = wave; pc < 2 * pieces; pc += 8) {
+    for (int pc = wave; pc < 2 * pieces; pc += nw) {
       const bool isv = pc >= pieces;
       const int piece = isv ? pc - pieces : pc;
       const int row = piece * 8 + prow;
@@ -225,40 +232,28 @@ __global__ __launch_bounds__(512) void attention_pipe_kernel(const T* __restrict
     }
   };
 
+  i16x8 qf[4], qn[4];
   stage(bh0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
+  load_q<T>(qf, head_base(bh0), ld, wave, N, lane);
   for (int j = 0; j < nh; ++j) {
     const int bh = bh0 + j, b = bh / H, h = bh - b * H;
-    const T* base = qkv + (size_t)b * N * ld + h * 64;
-    const char* kimg = smem + (j & 1) * 2 * img_bytes;
-    const char* vimg = kimg + img_bytes;
-    const int c0 = ((wave - j) % 8 + 8) % 8;     // first chunk of this wave for head j
-    // Q fragments of the wave's first chunk are loaded before the next head's
-    // LDS-DMA is issued, so waiting for them never waits for that DMA.
-    i16x8 qf[4];
-    if (c0 < nchunks) load_q<T>(qf, base, ld, c0, N, lane);
-    // retire the Q loads now, naming qf as outputs so hipcc sees them defined
-    // here: otherwise it waits vmcnt(0) at the first MFMA, i.e. for the whole
-    // next-head DMA issued below (guide §5.7 item 1, form (ii)).
+    // retire this wave's DMA of head j and its Q loads; qf named as outputs so
+    // hipcc sees it defined here (its own wait would be a vmcnt(0) at the
+    // first MFMA, i.e. after the next head's DMA is issued: guide §5.7 item 1)
     asm volatile("s_waitcnt vmcnt(0)"
                  : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])
                  :
                  : "memory");
-    if (j + 1 < nh) stage(bh + 1, (j + 1) & 1);
-    T* orow = out + (size_t)b * N * D + h * 64;
-    for (int c = c0; c < nchunks; c += 8) {
-      if (c != c0) {
-        load_q<T>(qf, base, ld, c, N, lane);
-        asm volatile("s_waitcnt vmcnt(0)"
-                     : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])
-                     :
-                     : "memory");
-      }
-      attend_chunk<T, CAUSAL>(kimg, vimg, qf, c, N, Npad, c2, orow, D, lane);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    if (j + 1 < nh) {
+      stage(bh + 1, (j + 1) & 1);
+      load_q<T>(qn, head_base(bh + 1), ld, wave, N, lane);
+    }
+    const char* kimg = smem + (j & 1) * 2 * img_bytes;
+    attend_chunk<T, CAUSAL>(kimg, kimg + img_bytes, qf, wave, N, Npad, c2,
+                            out + (size_t)b * N * D + h * 64, D, lane);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = qn[s];
   }
 }
 
@@ -279,11 +274,7 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, hipStrea
   const size_t lds = (size_t)Npad * 256;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (variant == 0) variant = attn_variant();
-  // pipelined kernel (opt-in, variant 2): two K/V buffers must fit in LDS
-  // (N <= 320). Measured slower at N = 257 (0.27 vs 0.24-0.26 ms per ViT-L
-  // layer): 9 query chunks on 8 waves leave one wave with two chunks before
-  // every per-head barrier, and 2 one-head workgroups per CU already overlap
-  // one head's K/V load with the other's compute.
+  // pipelined kernel (variant 2): two K/V buffers must fit in LDS (N <= 320)
   if (variant == 2 && 2 * lds <= 160 * 1024) {
     auto kern = attention_pipe_kernel<T, CAUSAL>;
     static bool attr_set = false;
@@ -293,13 +284,21 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, hipStrea
       if (e != hipSuccess) return e;
       attr_set = true;
     }
-    // enough workgroups to fill the chip twice, at most 8 heads each
-    const int heads = B * H;
-    int hpw = (heads + 511) / 512;
-    hpw = hpw < 1 ? 1 : (hpw > 8 ? 8 : hpw);
+    // one round of workgroups over the CUs at the occupancy LDS allows
+    static int ncu = [] {
+      int d = 0, n = 0;
+      if (hipGetDevice(&d) != hipSuccess ||
+          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+        n = 256;
+      return n;
+    }();
+    const int per_cu = (int)((160 * 1024) / (2 * lds)) < 1 ? 1 : (int)((160 * 1024) / (2 * lds));
+    const int heads = B * H, slots = ncu * per_cu;
+    int hpw = (heads + slots - 1) / slots;
+    hpw = hpw < 1 ? 1 : hpw;
     const int grid = (heads + hpw - 1) / hpw;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 2 * lds, s, (const T*)qkv, (T*)out, B, N, H,
-                       Npad, nchunks, hpw, 0.125f);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(nchunks * 64), 2 * lds, s, (const T*)qkv,
+                       (T*)out, B, N, H, Npad, hpw, 0.125f);
     return hipGetLastError();
   }
   const int per = (nchunks + 15) / 16;

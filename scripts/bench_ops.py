@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--ops", default="gemm,attention,layernorm")
     ap.add_argument("--ksweep", action="store_true", help="N=1024 GEMM at K=1024..8192")
     ap.add_argument("--only", default="", help="comma list of gemm shape names to run")
+    ap.add_argument("--torch", action="store_true", help="also time torch.nn.functional.linear")
     args = ap.parse_args()
     lib = _lib.load_library()
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -75,6 +76,15 @@ def main():
                 out.append(dict(op=f"gemm_{name}", variant=v, M=M, N=N, K=K, ms=round(ms, 4),
                                 tflops=round(fl / ms / 1e9, 1), gbs=round(by / ms / 1e6, 1)))
                 print(json.dumps(out[-1]), flush=True)
+        if args.torch:   # library reference point: torch -> hipBLASLt, same shapes, no epilogue
+            for name, N, K, epi, act in shapes:
+                a_, w_ = A[:, :K].contiguous(), Wt[:N, :K].contiguous()
+                ms = timeit(lambda: torch.nn.functional.linear(a_, w_), args.iters)
+                fl = 2.0 * M * N * K
+                out.append(dict(op=f"torch_{name}", M=M, N=N, K=K, ms=round(ms, 4),
+                                tflops=round(fl / ms / 1e9, 1)))
+                print(json.dumps(out[-1]), flush=True)
+                del a_, w_
         del A, Wt, C16, X
     if "attention" in args.ops:
         H = W // 64

@@ -24,6 +24,7 @@ for step in "${steps[@]}"; do
     ops)     run ops 300 python scripts/bench_ops.py --variants 258 ;;
     pre)     run pre 300 python -m pytest tests/test_preprocess.py -q -rf ;;
     benchpre) run benchpre 300 python scripts/bench_preprocess.py ;;
+    blas)    run blas 300 python scripts/bench_ops.py --ops gemm --variants 0 --torch ;;
     attn)    run attn 200 python scripts/bench_ops.py --ops attention ;;
     group)   run group 300 python scripts/bench_ops.py --ops gemm --variants 1258,4258,8258,2258,1258,4258 ;;
     traffic) run traffic 700 bash scripts/pmc.sh traffic ;;
