@@ -81,19 +81,29 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg, const i16x8 (&q
     // exceeds it by <= 8 (p <= 2^8, exact range for fp16/bf16 P).
     if (!__all(tmax - m <= 8.0f)) {
       const float mnew = fmaxf(m, tmax);
-      const float alpha = exp2f(m - mnew);
+      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
       m = mnew;
       lsum *= alpha;
 #pragma unroll
       for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
     }
-    float psum = 0.f;
+    // raw v_exp_f32: exp2f's denormal-range fix-up (cmp/cndmask/ldexp per
+    // element) is dead weight here -- results below 2^-126 vanish in the fp16
+    // P operand anyway. Four partial sums break the add dependency chain.
+    f32x2 ps0 = {0.f, 0.f}, ps1 = {0.f, 0.f};
+    const f32x2 c2v = {c2, c2}, mv = {-m, -m};
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      sacc[r] = exp2f(fmaf(sacc[r], c2, -m));
-      psum += sacc[r];
+    for (int r = 0; r < 16; r += 2) {
+      f32x2 v = {sacc[r], sacc[r + 1]};
+      v = __builtin_elementwise_fma(v, c2v, mv);          // v_pk_fma_f32
+      v[0] = __builtin_amdgcn_exp2f(v[0]);
+      v[1] = __builtin_amdgcn_exp2f(v[1]);
+      sacc[r] = v[0];
+      sacc[r + 1] = v[1];
+      if (r & 2) ps1 += v; else ps0 += v;                  // v_pk_add_f32
     }
-    lsum += psum;
+    ps0 += ps1;
+    lsum += ps0[0] + ps0[1];
     // ---- P^T as B operand: k-step s2 uses accumulator regs 8*s2 .. 8*s2+7 ----
     i16x8 pf[2];
 #pragma unroll
