@@ -133,8 +133,7 @@ struct miclip_model {
     double ms = 0, flops = 0, bytes = 0;
   };
   std::vector<ProfAcc> prof_acc;
-  miclip_image_desc* pre_desc = nullptr;   // device copy of miclip_preprocess descriptors
-  int pre_cap = 0;
+  PreCache* pre = nullptr;   // miclip_preprocess state (geometry tables, image array)
 };
 
 namespace {
@@ -589,24 +588,10 @@ int miclip_preprocess(miclip_model* m, const uint8_t* pixels, const miclip_image
                       int32_t B, void* out, int32_t out_kind, void* stream) {
   if (!m || !pixels || !descs || !out || B < 1)
     return fail(MICLIP_EINVAL, "bad argument to preprocess");
-  const hipStream_t s = (hipStream_t)stream;
-  if (B > m->pre_cap) {
-    if (m->pre_desc) {
-      MICLIP_HIP(hipStreamSynchronize(s));   // the old buffer may still be read
-      dev_free(m, m->pre_desc);
-      m->pre_desc = nullptr;
-      m->pre_cap = 0;
-    }
-    const int cap = B < 256 ? 256 : B;
-    if (int rc = dev_alloc(m, (void**)&m->pre_desc, sizeof(miclip_image_desc) * cap)) return rc;
-    m->pre_cap = cap;
-  }
+  if (!m->pre) m->pre = pre_cache_create();
   char err[256] = {0};
-  // pageable source: the copy has consumed `descs` when hipMemcpyAsync returns
-  MICLIP_HIP(hipMemcpyAsync(m->pre_desc, descs, sizeof(miclip_image_desc) * B,
-                            hipMemcpyHostToDevice, s));
-  const hipError_t e = preprocess(pixels, descs, m->pre_desc, B, m->cfg.image_resolution,
-                                  out_kind, out, s, err, sizeof(err));
+  const hipError_t e = preprocess(m->pre, pixels, descs, B, m->cfg.image_resolution, out_kind,
+                                  out, (hipStream_t)stream, err, sizeof(err));
   if (e != hipSuccess)
     return fail(e == hipErrorInvalidValue ? MICLIP_EINVAL : MICLIP_EHIP,
                 err[0] ? std::string(err) : std::string("preprocess: ") + hipGetErrorString(e));
@@ -659,6 +644,7 @@ void miclip_model_destroy(miclip_model* m) {
     if (m->ev_join[i]) (void)hipEventDestroy(m->ev_join[i]);
     if (m->aux[i]) (void)hipStreamDestroy(m->aux[i]);
   }
+  pre_cache_destroy(m->pre);
   for (auto& kv : m->allocs) (void)hipFree(kv.first);
   delete m;
 }

@@ -42,8 +42,9 @@ hipError_t layernorm(int dtype, const float* in, const int32_t* rows, int in_str
 // ---- fused multi-head attention over a packed QKV buffer ----
 // qkv: [B*N, 3*H*64] compute dtype (torch in_proj order q|k|v); out: [B*N, H*64].
 // head dim 64; causal adds the -inf strictly-upper-triangular mask (clip/model.py:323-329).
-// variant: 0 = default (MICLIP_ATTN env, else one head per workgroup),
-// 1 = one head per workgroup, 2 = pipelined multi-head kernel (N <= 320).
+// variant: 0 = default (MICLIP_ATTN env, else the pipelined multi-head kernel
+// when N <= 320, one head per workgroup above), 1 = one head per workgroup,
+// 2 = pipelined.
 hipError_t attention(int dtype, const void* qkv, void* out, int B, int N, int H, int causal,
                      hipStream_t s, int variant = 0);
 
@@ -71,11 +72,14 @@ hipError_t zero_shot(const float* x, const float* proj, const float* tw, float* 
                      hipStream_t s);
 
 // ---- on-device CLIP preprocessing (bicubic resize + center crop + normalise) ----
-// descs_host / descs_dev: the same B descriptors on host (validated, sizes the
-// launch) and in device memory (read by the kernel); out_kind 0 = float32
-// [B,3,n,n] normalised, 1 = uint8 [B,n,n,3]. On error fills `err`.
-hipError_t preprocess(const uint8_t* pixels, const miclip_image_desc* descs_host,
-                      const miclip_image_desc* descs_dev, int B, int n, int out_kind, void* out,
-                      hipStream_t s, char* err, int errlen);
+// PreCache: geometry-table cache + image-array buffers, one per model handle.
+// descs: HOST array of B descriptors (validated, copied stream-ordered);
+// out_kind 0 = float32 [B,3,n,n] normalised, 1 = uint8 [B,n,n,3]. On error
+// fills `err`.
+struct PreCache;
+PreCache* pre_cache_create();
+void pre_cache_destroy(PreCache* c);
+hipError_t preprocess(PreCache* c, const uint8_t* pixels, const miclip_image_desc* descs, int B,
+                      int n, int out_kind, void* out, hipStream_t s, char* err, int errlen);
 
 }  // namespace miclip

@@ -6,20 +6,28 @@
 //   -> Normalize(CLIP_MEAN, CLIP_STD)
 // whose arithmetic is torchvision's size/anchor rules over Pillow's
 // libImaging/Resample.c (8-bit two-pass separable cubic, a = -0.5, fixed point
-// with 22 fractional bits). The kernel reproduces it bit for bit on uint8 HWC
+// with 22 fractional bits). The kernels reproduce it bit for bit on uint8 HWC
 // images already in HBM, computing only the crop window:
-//   * coefficients are evaluated per workgroup in double with FP contraction
-//     off, in Resample.c's operation order (identical doubles to the CPU);
-//   * horizontal pass: input rows the band's vertical taps need x crop
-//     columns -> uint8 staging rows in LDS (clip8 between passes, as Pillow);
-//   * vertical pass from LDS -> clip8 -> float32 x/255, (x-mean)/std
-//     (ToTensor + Normalize) written planar [B,3,n,n], or the uint8 crop.
-// One workgroup per (image, band of 16 crop rows); the band's vertical span
-// is cut into sub-bands that fit the LDS staging area. HBM-bound: each input
-// byte of the crop window is read about once (L1/L2 absorb the tap overlap).
+//   * `pre_tables_kernel` evaluates, once per distinct (H, W, n) geometry, the
+//     crop window's horizontal and vertical coefficient tables in double with
+//     FP contraction off, in Resample.c's operation order (the same doubles
+//     the CPU computes), normalised to 22-bit fixed point; the handle caches
+//     them (PreCache);
+//   * `preprocess_kernel`, one workgroup per (image, band of 16 crop rows):
+//     horizontal pass over the input rows the band's vertical taps need x
+//     crop columns -> clip8 -> uint8 rows in LDS; vertical pass from LDS ->
+//     clip8 -> float32 x/255, (x-mean)/std written planar [B,3,n,n] (or the
+//     uint8 crop). Input pixels come through a per-image range-checked buffer
+//     descriptor, 16 B per load (4 RGB taps), realigned with v_alignbyte and
+//     accumulated with v_mad_i32_i24 (|coefficient| < 2^23, pixel < 2^8).
+// HBM-bound in principle (each byte of the crop window is read about once;
+// L1/L2 absorb the overlap of neighbouring taps).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+
+#include <map>
+#include <tuple>
 
 #include "miclip.h"
 #include "kernels.h"
@@ -29,7 +37,11 @@ namespace {
 
 constexpr int kPB = 22;          // Resample.c PRECISION_BITS = 32 - 8 - 2
 constexpr int kBand = 16;        // crop rows per workgroup
-constexpr int kThreads = 256;
+constexpr int kThreads = 1024;   // 16 waves: the horizontal pass is load-latency bound
+constexpr int kTmpBytes = 96 * 1024;   // LDS staging of horizontally resampled rows
+constexpr int kMaxTaps = 64;
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #pragma clang fp contract(off)
 __device__ __host__ double cubic(double x) {
@@ -41,10 +53,9 @@ __device__ __host__ double cubic(double x) {
 }
 
 // Resample.c precompute_coeffs + normalize_coeffs_8bpc for output index xx of
-// an in_size -> out_size resize over the whole input; writes ksize fixed-point
-// taps (zeros past the count) and returns (xmin, count).
-__device__ void coeffs(int in_size, int out_size, int xx, int ksize, int* k, int& xmin_out,
-                       int& cnt_out) {
+// an in_size -> out_size resize over the whole input: ksize fixed-point taps
+// (zeros past the count), returns (xmin, count).
+__device__ void coeffs(int in_size, int out_size, int xx, int ksize, int* k, int* bounds) {
   double filterscale, scale;
   filterscale = scale = (double)in_size / out_size;
   if (filterscale < 1.0) filterscale = 1.0;
@@ -68,13 +79,8 @@ __device__ void coeffs(int in_size, int out_size, int xx, int ksize, int* k, int
     }
     k[x] = v;
   }
-  xmin_out = xmin;
-  cnt_out = xmax;
-}
-
-__device__ __forceinline__ int clip8(int v) {
-  v >>= kPB;
-  return v < 0 ? 0 : (v > 255 ? 255 : v);
+  bounds[0] = xmin;
+  bounds[1] = xmax;
 }
 
 struct Geo {
@@ -83,7 +89,7 @@ struct Geo {
 
 // torchvision: short side -> n, long side -> int(n * long / short); crop anchor
 // int(round((size - n) / 2.0)) with Python's half-to-even round.
-__device__ __host__ Geo geometry(int h, int w, int n) {
+__host__ __device__ Geo geometry(int h, int w, int n) {
   Geo g;
   if (w <= h) {
     g.nw = n;
@@ -97,41 +103,102 @@ __device__ __host__ Geo geometry(int h, int w, int n) {
   return g;
 }
 
+int ksize_for(int in_size, int out_size) {
+  double fs = (double)in_size / out_size;
+  if (fs < 1.0) fs = 1.0;
+  return (int)ceil(2.0 * fs) * 2 + 1;
+}
+
+// Geometry table: [KH, KV, 0 x 6] | hb [n][2] | hk [n][KH] | vb [n][2] | vk [n][KV]
+int table_ints(int n, int KH, int KV) { return 8 + n * (4 + KH + KV); }
+
+__global__ __launch_bounds__(256) void pre_tables_kernel(int H, int W, int n, int KH,
+                                                              int KV, int* __restrict__ tab) {
+  const Geo g = geometry(H, W, n);
+  int* hb = tab + 8;
+  int* hk = hb + 2 * n;
+  int* vb = hk + n * KH;
+  int* vk = vb + 2 * n;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i == 0) {
+    tab[0] = KH;
+    tab[1] = KV;
+    for (int e = 2; e < 8; ++e) tab[e] = 0;
+  }
+  if (i < n)
+    coeffs(W, g.nw, g.left + i, KH, hk + i * KH, hb + 2 * i);
+  else if (i < 2 * n)
+    coeffs(H, g.nh, g.top + (i - n), KV, vk + (i - n) * KV, vb + 2 * (i - n));
+}
+
+// One image of a launch (device copy, built on the host per call).
+struct PreImage {
+  int64_t offset;     // byte offset of pixel (0, 0) from the pixels base
+  uint32_t extent;    // bytes from pixel (0, 0) to the end of the last pixel
+  int32_t H, W, C, stride;
+  int32_t tab;        // int offset of its geometry table
+};
+static_assert(sizeof(PreImage) == 32, "PreImage layout");
+
+__device__ __forceinline__ int clip8(int v) {
+  v >>= kPB;
+  return v < 0 ? 0 : (v > 255 ? 255 : v);
+}
+
+// d = a[23:0] * b[23:0] + c, signed 24-bit multiply at full VALU rate (hipcc
+// lowers a plain int multiply to the quarter-rate v_mul_lo_u32 here)
+__device__ __forceinline__ int mad24(int a, int b, int c) {
+  int d;
+  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
+__device__ __forceinline__ int byte_of(uint32_t w, int i) {
+  return (int)__builtin_amdgcn_ubfe(w, 8 * i, 8);
+}
+
 template <int OUT>  // 0: float32 normalised planar [B,3,n,n]; 1: uint8 crop [B,n,n,3]
 __global__ __launch_bounds__(kThreads) void preprocess_kernel(
-    const uint8_t* __restrict__ pix, const miclip_image_desc* __restrict__ descs, int n, int KH,
-    int KV, int tmp_bytes, void* __restrict__ out) {
+    const uint8_t* __restrict__ pix, const PreImage* __restrict__ imgs,
+    const int* __restrict__ tabs, int n, int KH, int KV, void* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  int* kh = (int*)smem;                      // [n][KH]
+  int* kh = (int*)smem;                      // [n][KH], KH % 16 == 0, zero-padded
   int* khb = kh + n * KH;                    // [n][2] xmin, count
   int* kv = khb + 2 * n;                     // [kBand][KV]
   int* kvb = kv + kBand * KV;                // [kBand][2]
   uint8_t* tmp = (uint8_t*)(kvb + 2 * kBand);
 
   const int b = blockIdx.x, i0 = blockIdx.y * kBand, tid = threadIdx.x;
-  const miclip_image_desc d = descs[b];
-  const int H = d.height, W = d.width, C = d.channels;
-  const int stride = d.row_stride ? d.row_stride : W * C;
-  const uint8_t* img = pix + d.offset;
-  const Geo g = geometry(H, W, n);
+  const PreImage d = imgs[b];
+  const int C = d.C, stride = d.stride;
+  const int* tab = tabs + d.tab;
+  const int KHg = tab[0], KVg = tab[1];
+  const int* hb = tab + 8;
+  const int* hk = hb + 2 * n;
+  const int* vb = hk + n * KHg;
+  const int* vk = vb + 2 * n;
   const int nrows = n - i0 < kBand ? n - i0 : kBand;
 
-  for (int j = tid; j < n; j += kThreads) {
-    int xmin, cnt;
-    coeffs(W, g.nw, g.left + j, KH, kh + j * KH, xmin, cnt);
-    khb[2 * j] = xmin;
-    khb[2 * j + 1] = cnt;
+  for (int e = tid; e < n * KH; e += kThreads) {
+    const int j = e / KH, t = e - j * KH;
+    kh[e] = t < KHg ? hk[j * KHg + t] : 0;
   }
-  for (int i = tid; i < nrows; i += kThreads) {
-    int ymin, cnt;
-    coeffs(H, g.nh, g.top + i0 + i, KV, kv + i * KV, ymin, cnt);
-    kvb[2 * i] = ymin;
-    kvb[2 * i + 1] = cnt;
+  for (int e = tid; e < 2 * n; e += kThreads) khb[e] = hb[e];
+  for (int e = tid; e < nrows * KV; e += kThreads) {
+    const int i = e / KV, t = e - i * KV;
+    kv[e] = t < KVg ? vk[(i0 + i) * KVg + t] : 0;
   }
+  for (int e = tid; e < 2 * nrows; e += kThreads) kvb[e] = vb[2 * i0 + e];
   __syncthreads();
 
+  // per-image range-checked descriptor: loads past the image read 0, never fault
+  const uint8_t* base = pix + d.offset;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)d.extent, 0x00020000);
+  const uint32_t extent = d.extent;
+
   const int rowb = n * C;                    // bytes of one staged row
-  const int cap = tmp_bytes / rowb;          // staged rows that fit
+  const int cap = kTmpBytes / rowb;          // staged rows that fit
   int s0 = 0;
   while (s0 < nrows) {
     // grow the sub-band while its input-row span fits the staging area
@@ -144,16 +211,52 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(
     // horizontal pass: staged[r][j][c] = clip8(half + sum_t in[ylo+r][xmin_j+t][c] * kh[j][t])
     for (int it = tid; it < rows * n; it += kThreads) {
       const int r = it / n, j = it - r * n;
-      const int xmin = khb[2 * j], cnt = khb[2 * j + 1];
+      const int cnt = khb[2 * j + 1];
       const int* k = kh + j * KH;
-      const uint8_t* p = img + (size_t)(ylo + r) * stride + (size_t)xmin * C;
+      const uint32_t voff = (uint32_t)(ylo + r) * stride + (uint32_t)khb[2 * j] * C;
+      const uint32_t al = voff & ~3u, sh = voff & 3u;
+      const int ng = (cnt + 3) >> 2;                // groups of 4 taps
       if (C == 3) {
         int a0 = 1 << (kPB - 1), a1 = a0, a2 = a0;
-        for (int t = 0; t < cnt; ++t) {
-          const int kt = k[t];
-          a0 += p[3 * t] * kt;
-          a1 += p[3 * t + 1] * kt;
-          a2 += p[3 * t + 2] * kt;
+        auto taps4 = [&](uint32_t w0, uint32_t w1, uint32_t w2, int4 kk) {
+          a0 = mad24(byte_of(w0, 0), kk.x, a0);
+          a1 = mad24(byte_of(w0, 1), kk.x, a1);
+          a2 = mad24(byte_of(w0, 2), kk.x, a2);
+          a0 = mad24(byte_of(w0, 3), kk.y, a0);
+          a1 = mad24(byte_of(w1, 0), kk.y, a1);
+          a2 = mad24(byte_of(w1, 1), kk.y, a2);
+          a0 = mad24(byte_of(w1, 2), kk.z, a0);
+          a1 = mad24(byte_of(w1, 3), kk.z, a1);
+          a2 = mad24(byte_of(w2, 0), kk.z, a2);
+          a0 = mad24(byte_of(w2, 1), kk.w, a0);
+          a1 = mad24(byte_of(w2, 2), kk.w, a1);
+          a2 = mad24(byte_of(w2, 3), kk.w, a2);
+        };
+        // fast path: every 16-B load of the item (4 groups per batch, the
+        // batch's surplus groups meet zero coefficients) lies inside the image
+        if (al + 48u * ((ng + 3) >> 2) + 16u <= extent) {
+          for (int g = 0; g < ng; g += 4) {
+            u32x4 v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              v[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, al + 12u * (g + q), 0, 0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              taps4(__builtin_amdgcn_alignbyte(v[q][1], v[q][0], sh),
+                    __builtin_amdgcn_alignbyte(v[q][2], v[q][1], sh),
+                    __builtin_amdgcn_alignbyte(v[q][3], v[q][2], sh),
+                    *(const int4*)(k + 4 * (g + q)));
+          }
+        } else {   // the image's last bytes: byte loads, each range-checked
+          for (int g = 0; g < ng; ++g) {
+            uint32_t bb[12];
+#pragma unroll
+            for (int e = 0; e < 12; ++e)
+              bb[e] = __builtin_amdgcn_raw_buffer_load_b8(rs, voff + 12u * g + e, 0, 0);
+            taps4(bb[0] | bb[1] << 8 | bb[2] << 16 | bb[3] << 24,
+                  bb[4] | bb[5] << 8 | bb[6] << 16 | bb[7] << 24,
+                  bb[8] | bb[9] << 8 | bb[10] << 16 | bb[11] << 24, *(const int4*)(k + 4 * g));
+          }
         }
         uint8_t* q = tmp + r * rowb + 3 * j;
         q[0] = (uint8_t)clip8(a0);
@@ -161,7 +264,32 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(
         q[2] = (uint8_t)clip8(a2);
       } else {
         int a0 = 1 << (kPB - 1);
-        for (int t = 0; t < cnt; ++t) a0 += p[t] * k[t];
+        auto taps4 = [&](uint32_t w, int4 kk) {
+          a0 = mad24(byte_of(w, 0), kk.x, a0);
+          a0 = mad24(byte_of(w, 1), kk.y, a0);
+          a0 = mad24(byte_of(w, 2), kk.z, a0);
+          a0 = mad24(byte_of(w, 3), kk.w, a0);
+        };
+        if (al + 16u * ((ng + 3) >> 2) + 8u <= extent) {
+          for (int g = 0; g < ng; g += 4) {
+            u32x4 v[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+              v[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, al + 4u * g + 8u * q, 0, 0);
+            taps4(__builtin_amdgcn_alignbyte(v[0][1], v[0][0], sh), *(const int4*)(k + 4 * g));
+            taps4(__builtin_amdgcn_alignbyte(v[0][2], v[0][1], sh), *(const int4*)(k + 4 * g + 4));
+            taps4(__builtin_amdgcn_alignbyte(v[0][3], v[0][2], sh), *(const int4*)(k + 4 * g + 8));
+            taps4(__builtin_amdgcn_alignbyte(v[1][2], v[1][1], sh), *(const int4*)(k + 4 * g + 12));
+          }
+        } else {
+          for (int g = 0; g < ng; ++g) {
+            uint32_t bb[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              bb[e] = __builtin_amdgcn_raw_buffer_load_b8(rs, voff + 4u * g + e, 0, 0);
+            taps4(bb[0] | bb[1] << 8 | bb[2] << 16 | bb[3] << 24, *(const int4*)(k + 4 * g));
+          }
+        }
         tmp[r * rowb + j] = (uint8_t)clip8(a0);
       }
     }
@@ -173,13 +301,23 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(
       const int ymin = kvb[2 * i] - ylo, cnt = kvb[2 * i + 1];
       const int* k = kv + i * KV;
       int u[3];
-      for (int c = 0; c < C; ++c) {
-        int a = 1 << (kPB - 1);
-        const uint8_t* q = tmp + ymin * rowb + j * C + c;
-        for (int t = 0; t < cnt; ++t) a += q[t * rowb] * k[t];
-        u[c] = clip8(a);
+      const uint8_t* q = tmp + ymin * rowb + j * C;
+      if (C == 3) {
+        int a0 = 1 << (kPB - 1), a1 = a0, a2 = a0;
+        for (int t = 0; t < cnt; ++t, q += rowb) {
+          const int kt = k[t];
+          a0 = mad24(q[0], kt, a0);
+          a1 = mad24(q[1], kt, a1);
+          a2 = mad24(q[2], kt, a2);
+        }
+        u[0] = clip8(a0);
+        u[1] = clip8(a1);
+        u[2] = clip8(a2);
+      } else {
+        int a0 = 1 << (kPB - 1);
+        for (int t = 0; t < cnt; ++t, q += rowb) a0 = mad24(q[0], k[t], a0);
+        u[0] = u[1] = u[2] = clip8(a0);   // convert("RGB") of an 'L' image
       }
-      if (C == 1) u[1] = u[2] = u[0];   // convert("RGB") of an 'L' image
       const int orow = i0 + i;
       if (OUT == 1) {
         uint8_t* o = (uint8_t*)out + (((size_t)b * n + orow) * n + j) * 3;
@@ -203,65 +341,147 @@ __global__ __launch_bounds__(kThreads) void preprocess_kernel(
   }
 }
 
-int ksize_for(int in_size, int out_size) {
-  double fs = (double)in_size / out_size;
-  if (fs < 1.0) fs = 1.0;
-  return (int)ceil(2.0 * fs) * 2 + 1;
+hipError_t set_lds_attr(const void* f) {
+  return hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
 
 }  // namespace
 
-constexpr int kPreTmpBytes = 96 * 1024;
+// Handle-owned state of miclip_preprocess: the geometry-table cache and the
+// per-call image array (pinned staging + device copy).
+struct PreCache {
+  struct Entry {
+    int off, KH, KV;
+  };
+  std::map<std::tuple<int, int, int>, Entry> geo;
+  int* tabs = nullptr;
+  size_t tab_cap = 0, tab_used = 0;   // ints
+  PreImage* dev_imgs = nullptr;
+  PreImage* host_imgs = nullptr;      // pinned
+  int img_cap = 0;
+  hipEvent_t copied = nullptr;        // last image-array upload done
+  bool copy_pending = false;
+};
 
-hipError_t preprocess(const uint8_t* pixels, const miclip_image_desc* descs_host,
-                      const miclip_image_desc* descs_dev, int B, int n, int out_kind, void* out,
-                      hipStream_t s, char* err, int errlen) {
-  if (B < 1 || n < 1 || n > 1024 || (out_kind != 0 && out_kind != 1)) {
+PreCache* pre_cache_create() { return new PreCache(); }
+
+void pre_cache_destroy(PreCache* c) {
+  if (!c) return;
+  if (c->copied) (void)hipEventSynchronize(c->copied);
+  if (c->tabs) (void)hipFree(c->tabs);
+  if (c->dev_imgs) (void)hipFree(c->dev_imgs);
+  if (c->host_imgs) (void)hipHostFree(c->host_imgs);
+  if (c->copied) (void)hipEventDestroy(c->copied);
+  delete c;
+}
+
+hipError_t preprocess(PreCache* c, const uint8_t* pixels, const miclip_image_desc* descs, int B,
+                      int n, int out_kind, void* out, hipStream_t s, char* err, int errlen) {
+  if (!c || B < 1 || n < 1 || n > 1024 || (out_kind != 0 && out_kind != 1)) {
     snprintf(err, errlen, "preprocess: bad batch %d / resolution %d / output kind %d", B, n,
              out_kind);
     return hipErrorInvalidValue;
   }
-  int KH = 1, KV = 1;
+  hipError_t e;
+  // validate, find or build each image's geometry table
+  int KH = 4, KV = 1;
+  if (B > c->img_cap) {
+    if (c->copy_pending && (e = hipEventSynchronize(c->copied)) != hipSuccess) return e;
+    c->copy_pending = false;
+    if (c->dev_imgs && (e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    if (c->dev_imgs) (void)hipFree(c->dev_imgs);
+    if (c->host_imgs) (void)hipHostFree(c->host_imgs);
+    c->dev_imgs = nullptr;
+    c->host_imgs = nullptr;
+    c->img_cap = 0;
+    const int cap = B < 256 ? 256 : B;
+    if ((e = hipMalloc(&c->dev_imgs, sizeof(PreImage) * cap)) != hipSuccess) return e;
+    if ((e = hipHostMalloc(&c->host_imgs, sizeof(PreImage) * cap)) != hipSuccess) return e;
+    c->img_cap = cap;
+  }
+  if (!c->copied && (e = hipEventCreateWithFlags(&c->copied, hipEventDisableTiming)) != hipSuccess)
+    return e;
+  if (c->copy_pending && (e = hipEventSynchronize(c->copied)) != hipSuccess) return e;
+  c->copy_pending = false;
   for (int i = 0; i < B; ++i) {
-    const miclip_image_desc& d = descs_host[i];
+    const miclip_image_desc& d = descs[i];
+    const int64_t stride = d.row_stride ? d.row_stride : (int64_t)d.width * d.channels;
+    const int64_t extent = (int64_t)(d.height - 1) * stride + (int64_t)d.width * d.channels;
     if (d.height < 1 || d.width < 1 || (d.channels != 1 && d.channels != 3) || d.offset < 0 ||
-        (d.row_stride != 0 && d.row_stride < d.width * d.channels)) {
+        stride < (int64_t)d.width * d.channels || extent >= (1ll << 32) - 16) {
       snprintf(err, errlen, "preprocess: image %d has an invalid descriptor (%dx%dx%d, stride %d)",
                i, d.height, d.width, d.channels, d.row_stride);
       return hipErrorInvalidValue;
     }
     const Geo g = geometry(d.height, d.width, n);
     const int kh = ksize_for(d.width, g.nw), kv = ksize_for(d.height, g.nh);
-    KH = kh > KH ? kh : KH;
-    KV = kv > KV ? kv : KV;
+    // a single crop row's vertical taps must fit the LDS staging area
+    if (kh > kMaxTaps || kv > kMaxTaps || kv > kTmpBytes / (n * 3)) {
+      snprintf(err, errlen,
+               "preprocess: image %d (%dx%d) downscales too far for resolution %d (taps %d x %d, "
+               "max %d)", i, d.height, d.width, n, kh, kv, kMaxTaps);
+      return hipErrorInvalidValue;
+    }
+    const auto key = std::make_tuple(d.height, d.width, n);
+    auto it = c->geo.find(key);
+    if (it == c->geo.end()) {
+      const size_t need = (size_t)table_ints(n, kh, kv);
+      if (c->tab_used + need > c->tab_cap) {
+        // grow (keeps every cached table: device-to-device copy, stream-ordered)
+        size_t cap = c->tab_cap ? 2 * c->tab_cap : (size_t)1 << 20;
+        while (cap < c->tab_used + need) cap *= 2;
+        int* nt = nullptr;
+        if ((e = hipMalloc(&nt, cap * sizeof(int))) != hipSuccess) return e;
+        if (c->tabs) {
+          if ((e = hipMemcpyAsync(nt, c->tabs, c->tab_used * sizeof(int),
+                                  hipMemcpyDeviceToDevice, s)) != hipSuccess)
+            return e;
+          if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+          (void)hipFree(c->tabs);
+        }
+        c->tabs = nt;
+        c->tab_cap = cap;
+      }
+      const int off = (int)c->tab_used;
+      hipLaunchKernelGGL(pre_tables_kernel, dim3((2 * n + 255) / 256),
+                         dim3(256), 0, s, d.height, d.width, n, kh, kv, c->tabs + off);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      c->tab_used += need;
+      it = c->geo.emplace(key, PreCache::Entry{off, kh, kv}).first;
+    }
+    KH = it->second.KH > KH ? it->second.KH : KH;
+    KV = it->second.KV > KV ? it->second.KV : KV;
+    PreImage& p = c->host_imgs[i];
+    p.offset = d.offset;
+    p.extent = (uint32_t)extent;
+    p.H = d.height;
+    p.W = d.width;
+    p.C = d.channels;
+    p.stride = (int32_t)stride;
+    p.tab = it->second.off;
   }
-  // a single crop row's vertical taps must fit the staging area
-  if (KH > 64 || KV > 64 || KV > kPreTmpBytes / (n * 3)) {
-    snprintf(err, errlen,
-             "preprocess: downscale factor too large for resolution %d (taps %d x %d, max 64)", n,
-             KH, KV);
-    return hipErrorInvalidValue;
-  }
-  const size_t lds = (size_t)(n * KH + 2 * n + kBand * KV + 2 * kBand) * 4 + kPreTmpBytes;
+  KH = (KH + 15) & ~15;   // batches of 4 groups of 4 taps read whole 16-int rows
+  const size_t lds = (size_t)(n * KH + 2 * n + kBand * KV + 2 * kBand) * 4 + kTmpBytes;
   if (lds > 160 * 1024) {
     snprintf(err, errlen, "preprocess: LDS need %zu B exceeds 160 KiB", lds);
     return hipErrorInvalidValue;
   }
+  if ((e = hipMemcpyAsync(c->dev_imgs, c->host_imgs, sizeof(PreImage) * B,
+                          hipMemcpyHostToDevice, s)) != hipSuccess)
+    return e;
+  if ((e = hipEventRecord(c->copied, s)) != hipSuccess) return e;
+  c->copy_pending = true;
   const dim3 grid(B, (n + kBand - 1) / kBand);
   if (out_kind == 0) {
-    static bool attr0 = hipFuncSetAttribute((const void*)preprocess_kernel<0>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            160 * 1024) == hipSuccess;
-    (void)attr0;
-    hipLaunchKernelGGL(preprocess_kernel<0>, grid, dim3(kThreads), lds, s, pixels, descs_dev, n,
-                       KH, KV, kPreTmpBytes, out);
+    static const hipError_t a0 = set_lds_attr((const void*)preprocess_kernel<0>);
+    if (a0 != hipSuccess) return a0;
+    hipLaunchKernelGGL(preprocess_kernel<0>, grid, dim3(kThreads), lds, s, pixels, c->dev_imgs,
+                       c->tabs, n, KH, KV, out);
   } else {
-    static bool attr1 = hipFuncSetAttribute((const void*)preprocess_kernel<1>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            160 * 1024) == hipSuccess;
-    (void)attr1;
-    hipLaunchKernelGGL(preprocess_kernel<1>, grid, dim3(kThreads), lds, s, pixels, descs_dev, n,
-                       KH, KV, kPreTmpBytes, out);
+    static const hipError_t a1 = set_lds_attr((const void*)preprocess_kernel<1>);
+    if (a1 != hipSuccess) return a1;
+    hipLaunchKernelGGL(preprocess_kernel<1>, grid, dim3(kThreads), lds, s, pixels, c->dev_imgs,
+                       c->tabs, n, KH, KV, out);
   }
   return hipGetLastError();
 }

@@ -187,8 +187,8 @@ int miclip_op_layernorm(int32_t dtype, const float* in, const float* gamma, cons
 /* softmax(Q K^T / 8 + mask) V per head over a packed qkv [B*N, 3*H*64] buffer,
  * out [B*N, H*64]; replaces F.scaled_dot_product_attention inside
  * nn.MultiheadAttention (clip/model.py:179-181), causal = text mask (323-329).
- * variant: 0 = default (one head per workgroup), 1 = the same, 2 = pipelined
- * multi-head kernel (N <= 320, diagnostic A/B). */
+ * variant: 0 = default (pipelined multi-head kernel for N <= 320, else one
+ * head per workgroup), 1 = one head per workgroup, 2 = pipelined. */
 int miclip_op_attention(int32_t dtype, const void* qkv, void* out, int32_t B, int32_t N,
                         int32_t H, int32_t causal, int32_t variant, void* stream);
 
