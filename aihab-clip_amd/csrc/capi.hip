@@ -134,6 +134,8 @@ struct miclip_model {
   };
   std::vector<ProfAcc> prof_acc;
   PreCache* pre = nullptr;   // miclip_preprocess state (geometry tables, image array)
+  float* zs_scratch = nullptr;   // zero-shot projected rows [B, embed_dim]
+  int64_t zs_cap = 0;
 };
 
 namespace {
@@ -579,8 +581,20 @@ int miclip_zero_shot(miclip_model* m, const float* feats, int32_t B, int32_t app
     return fail(MICLIP_ENOWEIGHTS, "visual.proj not loaded");
   const int E = m->cfg.embed_dim;
   const int Din = apply_proj ? m->cfg.vision_width : E;
+  if (apply_proj && (int64_t)B * E > m->zs_cap) {
+    if (m->zs_scratch) {
+      MICLIP_HIP(hipStreamSynchronize((hipStream_t)stream));   // may still be read
+      dev_free(m, m->zs_scratch);
+      m->zs_scratch = nullptr;
+      m->zs_cap = 0;
+    }
+    const int64_t cap = (int64_t)(B < 256 ? 256 : B) * E;
+    if (int rc = dev_alloc(m, (void**)&m->zs_scratch, sizeof(float) * cap)) return rc;
+    m->zs_cap = cap;
+  }
   MICLIP_HIP(zero_shot(feats, apply_proj ? m->vproj : nullptr, text_weights, logits,
-                       topk, B, Din, E, C, scale, topk ? k : 0, (hipStream_t)stream));
+                       topk, B, Din, E, C, scale, topk ? k : 0, (hipStream_t)stream,
+                       apply_proj ? m->zs_scratch : nullptr));
   return 0;
 }
 

@@ -94,8 +94,63 @@ __global__ __launch_bounds__(256) void rowvec_matmul_kernel(const float* __restr
   out[(size_t)r * E + e] = acc;
 }
 
-// ROWS images per workgroup: every visual.proj element read from L2 feeds ROWS
-// FMAs (the projection is the only real work: 2*Din*E flops per image).
+// out[b, e] = sum_d x[b, d] * W[d, e] (fp32), ROWS rows x 64 columns per
+// workgroup: each W element read (coalesced, 256 B per wave) feeds ROWS FMAs;
+// the 4 waves split d into quarters and the partials are summed in a fixed
+// order (deterministic). Grid: (ceil(B/ROWS), ceil(E/64)) -- enough workgroups
+// to spread visual.proj over the chip (B=256, E=768: 384 workgroups).
+template <int ROWS>
+__global__ __launch_bounds__(256) void rows_matmul_kernel(const float* __restrict__ x,
+                                                          const float* __restrict__ W,
+                                                          float* __restrict__ out, int B,
+                                                          int Din, int E) {
+  extern __shared__ float sm[];
+  float* xs = sm;                   // [ROWS][Din]
+  float* red = xs + ROWS * Din;     // [4][ROWS][64]
+  const int b0 = blockIdx.x * ROWS, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nr = B - b0 < ROWS ? B - b0 : ROWS;
+  const int col = blockIdx.y * 64 + lane;
+  for (int i = tid; i < ROWS * Din; i += 256) {
+    const int r = i / Din;
+    xs[i] = r < nr ? x[(size_t)(b0 + r) * Din + (i - r * Din)] : 0.f;
+  }
+  __syncthreads();
+  float acc[ROWS];
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r) acc[r] = 0.f;
+  const int q = (Din + 3) / 4, d0 = w * q, d1 = d0 + q < Din ? d0 + q : Din;
+  if (col < E) {
+    int d = d0;
+    for (; d + 8 <= d1; d += 8) {
+      float wv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) wv[u] = W[(size_t)(d + u) * E + col];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) acc[r] = fmaf(xs[r * Din + d + u], wv[u], acc[r]);
+    }
+    for (; d < d1; ++d) {
+      const float wv = W[(size_t)d * E + col];
+#pragma unroll
+      for (int r = 0; r < ROWS; ++r) acc[r] = fmaf(xs[r * Din + d], wv, acc[r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r) red[(w * ROWS + r) * 64 + lane] = acc[r];
+  __syncthreads();
+  for (int i = tid; i < nr * 64; i += 256) {
+    const int r = i >> 6, c = i & 63;
+    if (blockIdx.y * 64 + c < E)
+      out[(size_t)(b0 + r) * E + blockIdx.y * 64 + c] =
+          (red[(0 * ROWS + r) * 64 + c] + red[(1 * ROWS + r) * 64 + c]) +
+          (red[(2 * ROWS + r) * 64 + c] + red[(3 * ROWS + r) * 64 + c]);
+  }
+}
+
+// ROWS images per workgroup: L2-normalise, logits = scale * f @ tw, top-k. With
+// proj != null the projection runs here too (only used when the caller gives
+// no scratch for rows_matmul_kernel).
 template <int ROWS>
 __global__ __launch_bounds__(256) void zero_shot_kernel(const float* __restrict__ x,
                                                         const float* __restrict__ proj,
@@ -151,7 +206,15 @@ __global__ __launch_bounds__(256) void zero_shot_kernel(const float* __restrict_
     const int r = i / C, c = i - r * C;
     const float inv = red[ROWS * 4 + r];
     float acc = 0.f;
-    for (int e = 0; e < E; ++e) acc = fmaf(fs[r * E + e] * inv, tw[(size_t)e * C + c], acc);
+    int e = 0;
+    for (; e + 8 <= E; e += 8) {
+      float tv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) tv[u] = tw[(size_t)(e + u) * C + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = fmaf(fs[r * E + e + u] * inv, tv[u], acc);
+    }
+    for (; e < E; ++e) acc = fmaf(fs[r * E + e] * inv, tw[(size_t)e * C + c], acc);
     ls[r * C + c] = scale * acc;
     logits[(size_t)(b0 + r) * C + c] = scale * acc;
   }
@@ -219,6 +282,11 @@ hipError_t token_embed(const int64_t* tokens, const float* tok_emb, const float*
 hipError_t rowvec_matmul(const float* in, const float* Wm, float* out, int R, int D, int E,
                          hipStream_t s) {
   if (R < 1 || D < 1 || E < 1) return hipErrorInvalidValue;
+  if ((size_t)(8 * D + 4 * 8 * 64) * sizeof(float) <= 64 * 1024) {
+    hipLaunchKernelGGL(rows_matmul_kernel<8>, dim3((R + 7) / 8, (E + 63) / 64), dim3(256),
+                       (size_t)(8 * D + 4 * 8 * 64) * sizeof(float), s, in, Wm, out, R, D, E);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(rowvec_matmul_kernel, dim3((E + 255) / 256, R), dim3(256),
                      D * sizeof(float), s, in, Wm, out, D, E);
   return hipGetLastError();
@@ -226,8 +294,17 @@ hipError_t rowvec_matmul(const float* in, const float* Wm, float* out, int R, in
 
 hipError_t zero_shot(const float* x, const float* proj, const float* tw, float* logits,
                      int32_t* topk, int B, int Din, int E, int C, float scale, int k,
-                     hipStream_t s) {
+                     hipStream_t s, float* scratch) {
   if (B < 1 || C < 1 || E < 1 || k < 0 || k > C || (!proj && Din != E)) return hipErrorInvalidValue;
+  if (proj && scratch && (size_t)8 * Din * 4 + 4 * 8 * 64 * 4 <= 64 * 1024) {
+    // projection spread over the chip, then the head on the projected rows
+    hipLaunchKernelGGL(rows_matmul_kernel<8>, dim3((B + 7) / 8, (E + 63) / 64), dim3(256),
+                       (size_t)(8 * Din + 4 * 8 * 64) * sizeof(float), s, x, proj, scratch, B,
+                       Din, E);
+    x = scratch;
+    proj = nullptr;
+    Din = E;
+  }
   const size_t per_row = (size_t)(Din + E + C + 5) * sizeof(float);
   if (8 * per_row <= 64 * 1024) {
     hipLaunchKernelGGL(zero_shot_kernel<8>, dim3((B + 7) / 8), dim3(256), 8 * per_row, s, x, proj,

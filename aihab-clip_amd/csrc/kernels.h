@@ -67,9 +67,11 @@ hipError_t rowvec_matmul(const float* in, const float* Wm, float* out, int R, in
 hipError_t row_l2norm(float* x, int R, int D, hipStream_t s);
 // zero-shot head: f = normalize(x @ proj) (proj may be null -> f = normalize(x));
 // logits = scale * f @ tw ([E, C]); topk indices (sorted, largest first).
+// scratch (optional, fp32 [B, E]): the projection then runs as its own
+// chip-wide kernel (rows_matmul) before the head.
 hipError_t zero_shot(const float* x, const float* proj, const float* tw, float* logits,
                      int32_t* topk, int B, int Din, int E, int C, float scale, int k,
-                     hipStream_t s);
+                     hipStream_t s, float* scratch = nullptr);
 
 // ---- on-device CLIP preprocessing (bicubic resize + center crop + normalise) ----
 // PreCache: geometry-table cache + image-array buffers, one per model handle.

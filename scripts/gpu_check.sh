@@ -28,7 +28,7 @@ for step in "${steps[@]}"; do
     attn)    run attn 200 python scripts/bench_ops.py --ops attention ;;
     group)   run group 300 python scripts/bench_ops.py --ops gemm --variants 1258,4258,8258,2258,1258,4258 ;;
     traffic) run traffic 700 bash scripts/pmc.sh traffic ;;
-    ksweep)  run ksweep 300 python scripts/bench_ops.py --variants 256,258 --ksweep --ops gemm ;;
+    ksweep)  run ksweep 300 python scripts/bench_ops.py --variants 0 --ksweep --ops gemm ;;
     prof)    export TMPDIR=/tmp
              run prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
                  -d "$PWD/gpurun_out/prof" -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
