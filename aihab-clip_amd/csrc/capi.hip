@@ -612,6 +612,33 @@ int miclip_preprocess(miclip_model* m, const uint8_t* pixels, const miclip_image
   return 0;
 }
 
+int miclip_row_norms(const float* x, int32_t N, int32_t D, float* norms, float eps, float* out,
+                     void* stream) {
+  if (!x || !norms) return fail(MICLIP_EINVAL, "null argument");
+  MICLIP_HIP(row_norms(x, N, D, norms, (hipStream_t)stream));
+  if (out) MICLIP_HIP(div_rows(x, norms, N, D, eps, out, (hipStream_t)stream));
+  return 0;
+}
+
+int miclip_class_centroids(const float* x, const int32_t* order, const int32_t* offsets,
+                           int32_t K, int32_t D, float eps, float* sums, float* centroids,
+                           void* stream) {
+  if (!x || !order || !offsets || !sums || !centroids) return fail(MICLIP_EINVAL, "null argument");
+  MICLIP_HIP(class_centroids(x, order, offsets, K, D, eps, sums, centroids, (hipStream_t)stream));
+  return 0;
+}
+
+int miclip_proto_scores(const float* x, const float* protos, const int32_t* owner,
+                        const int32_t* cls, const float* inv_nx, const float* inv_np, int32_t N,
+                        int32_t P, int32_t D, float* own_best, int32_t* own_arg,
+                        float* other_best, void* stream) {
+  if (!x || !protos || !owner || !cls || !own_best || !own_arg || !other_best)
+    return fail(MICLIP_EINVAL, "null argument");
+  MICLIP_HIP(proto_scores(x, protos, owner, cls, inv_nx, inv_np, N, P, D, own_best, own_arg,
+                          other_best, (hipStream_t)stream));
+  return 0;
+}
+
 int miclip_set_profiling(miclip_model* m, int enable) {
   if (!m) return fail(MICLIP_EINVAL, "null model");
   m->profiling = enable != 0;

@@ -73,6 +73,23 @@ hipError_t zero_shot(const float* x, const float* proj, const float* tw, float* 
                      int32_t* topk, int B, int Din, int E, int C, float scale, int k,
                      hipStream_t s, float* scratch = nullptr);
 
+// ---- cached-feature consumers (outlier scoring), fp32 ----
+// norms[r] = ||x[r]||; out = x / max(norms, eps) per row.
+hipError_t row_norms(const float* x, int N, int D, float* norms, hipStream_t s);
+hipError_t div_rows(const float* x, const float* norms, int N, int D, float eps, float* out,
+                    hipStream_t s);
+// class k's rows are order[offsets[k] .. offsets[k+1]) (ascending sample order);
+// sums [K,D] = per-class sums in that order; centroids = normalize(sums / count).
+hipError_t class_centroids(const float* x, const int32_t* order, const int32_t* offsets, int K,
+                           int D, float eps, float* sums, float* centroids, hipStream_t s);
+// sim[s,p] = (x[s] . protos[p]) * inv_nx[s] * inv_np[p] (null -> 1); per sample:
+// own_best / own_arg = max / first argmax over p with owner[p] == cls[s],
+// other_best = max over the other prototypes (-inf when none).
+hipError_t proto_scores(const float* x, const float* protos, const int32_t* owner,
+                        const int32_t* cls, const float* inv_nx, const float* inv_np, int N,
+                        int P, int D, float* own_best, int32_t* own_arg, float* other_best,
+                        hipStream_t s);
+
 // ---- on-device CLIP preprocessing (bicubic resize + center crop + normalise) ----
 // PreCache: geometry-table cache + image-array buffers, one per model handle.
 // descs: HOST array of B descriptors (validated, copied stream-ordered);

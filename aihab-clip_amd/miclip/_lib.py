@@ -23,6 +23,7 @@ EXPORTS = (
     "miclip_model_destroy", "miclip_last_error", "miclip_abi_version",
     "miclip_model_bytes", "miclip_set_profiling", "miclip_profile_read", "miclip_set_splits",
     "miclip_op_gemm", "miclip_op_layernorm", "miclip_op_attention", "miclip_preprocess",
+    "miclip_row_norms", "miclip_class_centroids", "miclip_proto_scores",
 )
 
 MICLIP_PRE_F32 = 0
@@ -88,6 +89,10 @@ def load_library(path: str = None):
         "miclip_op_attention": ([i32, vp, vp, i32, i32, i32, i32, i32, vp], ctypes.c_int),
         "miclip_preprocess": ([vp, vp, ctypes.POINTER(MiclipImageDesc), i32, vp, i32, vp],
                               ctypes.c_int),
+        "miclip_row_norms": ([vp, i32, i32, vp, f32, vp, vp], ctypes.c_int),
+        "miclip_class_centroids": ([vp, vp, vp, i32, i32, f32, vp, vp, vp], ctypes.c_int),
+        "miclip_proto_scores": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp],
+                                ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

@@ -136,6 +136,31 @@ enum miclip_pre_out {
 int miclip_preprocess(miclip_model* m, const uint8_t* pixels, const miclip_image_desc* descs,
                       int32_t B, void* out, int32_t out_kind, void* stream);
 
+/* ---- cached-feature consumers: outlier scoring, fp32 ----
+ * Replace the torch ops of tools/outlier_cleaning.py's scorers on the
+ * embeddings cache; all pointers are device memory, calls stream-ordered.
+ * miclip_row_norms: norms[N] = emb.norm(dim=-1) (outlier_cleaning.py:234);
+ * with out != NULL also out = emb / max(norms, eps) (:244). */
+int miclip_row_norms(const float* x, int32_t N, int32_t D, float* norms, float eps, float* out,
+                     void* stream);
+/* Per-class normalised centroids (compute_centroids, :266-276): class k's
+ * rows are order[offsets[k] .. offsets[k+1]) in ascending sample order (a
+ * stable sort of the labels), summed in that order -- bit-identical to the
+ * CPU index_add_ -- then means = sums / count, F.normalize(eps).
+ * sums: scratch [K, D]; centroids: [K, D]. */
+int miclip_class_centroids(const float* x, const int32_t* order, const int32_t* offsets,
+                           int32_t K, int32_t D, float eps, float* sums, float* centroids,
+                           void* stream);
+/* Nearest-prototype scores (score_prototype_distance, :626-673; with inverse
+ * norms the cosine of score_centroid_distance, :329): sim = x . proto *
+ * inv_nx[s] * inv_np[p] (either may be NULL = 1); own_best / own_arg = best
+ * similarity and first best prototype index among owner[p] == cls[s];
+ * other_best = best over the other prototypes (-inf when there are none). */
+int miclip_proto_scores(const float* x, const float* protos, const int32_t* owner,
+                        const int32_t* cls, const float* inv_nx, const float* inv_np, int32_t N,
+                        int32_t P, int32_t D, float* own_best, int32_t* own_arg,
+                        float* other_best, void* stream);
+
 /* Batch split of encode_image over the caller's stream and one handle-owned
  * stream (fork/join by events, so the call stays stream-ordered and
  * graph-capturable): 1 = off, 2..4 = that many parts (default 2; a part is

@@ -22,6 +22,7 @@ for step in "${steps[@]}"; do
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   run bench 600 python bench.py --steps 10 --warmup 3 ;;
     ops)     run ops 300 python scripts/bench_ops.py --variants 258 ;;
+    outl)    run outl 300 python -m pytest tests/test_outliers.py -q -rf ;;
     pre)     run pre 300 python -m pytest tests/test_preprocess.py -q -rf ;;
     benchpre) run benchpre 300 python scripts/bench_preprocess.py ;;
     blas)    run blas 300 python scripts/bench_ops.py --ops gemm --variants 0 --torch ;;
