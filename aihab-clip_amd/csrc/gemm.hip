@@ -265,7 +265,56 @@ MICLIP_DEV void lds_barrier() {
 // SCHED 0: the half-tile schedule above (4 barriers per K-tile, ~1.5 K-tiles
 // in flight, fragment reads right after each barrier). SCHED 1: fragment
 // prefetch one quadrant ahead, one barrier per K-tile (see the branch below).
-template <typename T, class Epi, int SCHED>
+// 4x4 transpose inside each quad of lanes (DPP quad_perm): on entry lane jj of
+// a quad holds column jj of a 4x4 block (a[r] = M[r][jj], the MFMA C layout);
+// on exit it holds row jj (v[c] = M[jj][c]), i.e. 4 consecutive columns.
+template <int CTRL>
+MICLIP_DEV float dpp_f(float x) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
+}
+
+MICLIP_DEV float4 quad_transpose(f32x4 a, int lane) {
+  const bool odd = lane & 1, hi = lane & 2;
+  // stage 1, partner jj^1 (quad_perm [1,0,3,2]): even lanes end with rows {0,2},
+  // odd with rows {1,3}, each as a column pair (2u, 2u+1), u = jj >> 1
+  const float t0 = dpp_f<0xB1>(odd ? a[0] : a[1]);
+  const float t1 = dpp_f<0xB1>(odd ? a[2] : a[3]);
+  const float x0 = odd ? t0 : a[0], y0 = odd ? a[1] : t0;
+  const float x1 = odd ? t1 : a[2], y1 = odd ? a[3] : t1;
+  // stage 2, partner jj^2 (quad_perm [2,3,0,1]): u = 0 keeps its low row, u = 1 its high
+  const float r0 = dpp_f<0x4E>(hi ? x0 : x1);
+  const float r1 = dpp_f<0x4E>(hi ? y0 : y1);
+  return hi ? make_float4(r0, r1, x1, y1) : make_float4(x0, y0, r0, r1);
+}
+
+// Epilogue straight from the accumulators (no LDS): after the quad transpose
+// each lane owns 4 consecutive columns of one row of every 16x16 fragment, so
+// the epilogue functor's put4 (16-B aligned) applies unchanged. Rows are
+// m0 + wr*128 + qi*64 + i*16 + fk*4 + jj, columns n0 + wc*64 + qj*32 + j*16 + 4q.
+template <class Epi>
+MICLIP_DEV void epilogue_regs(const f32x4 (&acc)[2][2][4][2], int m0, int n0, int wr, int wc,
+                              int lane, int M, const Epi& epi) {
+  const int fk = lane >> 4, q = (lane & 15) >> 2, jj = lane & 3;
+  const bool full = m0 + 256 <= M;
+#pragma unroll
+  for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wc * 64 + qj * 32 + j * 16 + 4 * q;
+      const float4 bv = epi.bias4(col);
+#pragma unroll
+      for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float4 v = quad_transpose(acc[qi][qj][i][j], lane);
+          const int row = m0 + wr * 128 + qi * 64 + i * 16 + fk * 4 + jj;
+          if (full || row < M) epi.put4(row, col, v, bv);
+        }
+    }
+}
+
+template <typename T, class Epi, int SCHED, bool REGEPI = false>
 __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
                                                       const T* __restrict__ W, int M, int N,
                                                       int K, Epi epi, int gm) {
@@ -509,6 +558,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
     }
   }
 
+  if constexpr (REGEPI) {
+    epilogue_regs(acc, m0, n0, wr, wc, lane, M, epi);
+    return;
+  }
   // Epilogue through LDS: two passes (quadrant row qi), each stages the WG's
   // 128 x 256 fp32 accumulator rows {wr*128 + qi*64 + 0..63} in LDS (row stride
   // 260 floats: the 4 fk row groups of a ds_write_b32 land on distinct banks),
@@ -902,7 +955,7 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   variant %= 1000;
   if (variant == 0) variant = gemm_variant();
   if (variant != 0 && variant != 128 && variant != 256 && variant != 257 && variant != 258 &&
-      variant != 2 && variant != 3)
+      variant != 260 && variant != 2 && variant != 3)
     return hipErrorInvalidValue;
   if (variant == 3) {   // persistent 256x256
     static int ncu = [] {
@@ -931,7 +984,10 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   const int tiles256 = ((M + 255) / 256) * (N / 256);
   if (N % 256 == 0 && variant != 128 && (tiles256 >= 256 || variant >= 256)) {
     // default: the staggered schedule (SCHED 2); 256 / 257 select SCHED 0 / 1
-    if (variant == 257)
+    if (variant == 260)
+      hipLaunchKernelGGL((gemm256_kernel<T, Epi, 2, true>), dim3(tiles256), dim3(512), 0, s,
+                         (const T*)A, (const T*)W, M, N, K, epi, gm);
+    else if (variant == 257)
       hipLaunchKernelGGL((gemm256_kernel<T, Epi, 1>), dim3(tiles256), dim3(512), 0, s,
                          (const T*)A, (const T*)W, M, N, K, epi, gm);
     else if (variant == 256)

@@ -39,7 +39,9 @@ def _check(lib, rc):
                                           (1000, 768, 3072, 3), (300, 256, 192, 3), (257, 512, 64, 3),
                                           (65792, 1024, 128, 3), (2000, 2304, 256, 3),
                                           (1000, 768, 3072, 258), (300, 256, 192, 258), (257, 512, 64, 258),
-                                          (4096, 1024, 1024, 258), (33, 2304, 128, 258)])
+                                          (4096, 1024, 1024, 258), (33, 2304, 128, 258),
+                                          (1000, 768, 3072, 260), (300, 256, 192, 260), (257, 512, 64, 260),
+                                          (4096, 1024, 1024, 260), (33, 2304, 128, 260)])
 @pytest.mark.parametrize("epi,act", [(0, 0), (0, 1), (0, 2), (1, 0), (2, 0)])
 def test_gemm(lib, dt, M, N, K, variant, epi, act):
     code, tdt = DT[dt]
