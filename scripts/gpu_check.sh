@@ -25,7 +25,7 @@ for step in "${steps[@]}"; do
     outl)    run outl 300 python -m pytest tests/test_outliers.py -q -rf ;;
     pre)     run pre 300 python -m pytest tests/test_preprocess.py -q -rf ;;
     benchpre) run benchpre 300 python scripts/bench_preprocess.py ;;
-    regepi)  run regepi 300 python scripts/bench_ops.py --ops gemm --variants 0,260,0,260 ;;
+    regepi)  run regepi 300 python scripts/bench_ops.py --ops gemm --variants 0,260,3,0,260,3 ;;
     blas)    run blas 300 python scripts/bench_ops.py --ops gemm --variants 0 --torch ;;
     attn)    run attn 200 python scripts/bench_ops.py --ops attention ;;
     group)   run group 300 python scripts/bench_ops.py --ops gemm --variants 1258,4258,8258,2258,1258,4258 ;;

@@ -38,6 +38,7 @@ def _check(lib, rc):
                                           (33, 2304, 768, 257), (600, 1024, 4096, 257),
                                           (1000, 768, 3072, 3), (300, 256, 192, 3), (257, 512, 64, 3),
                                           (65792, 1024, 128, 3), (2000, 2304, 256, 3),
+                                          (65792, 1024, 1024, 3), (700, 2048, 320, 3),
                                           (1000, 768, 3072, 258), (300, 256, 192, 258), (257, 512, 64, 258),
                                           (4096, 1024, 1024, 258), (33, 2304, 128, 258),
                                           (1000, 768, 3072, 260), (300, 256, 192, 260), (257, 512, 64, 260),
