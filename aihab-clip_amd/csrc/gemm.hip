@@ -1115,7 +1115,12 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   // small ones (text tower, tiny batches) keep more workgroups with 128x128.
   const int tiles256 = ((M + 255) / 256) * (N / 256);
   if (N % 256 == 0 && variant != 128 && (tiles256 >= 256 || variant >= 256)) {
-    // default: the staggered schedule (SCHED 2); 256 / 257 select SCHED 0 / 1
+    // default: the staggered schedule (SCHED 2) with the LDS-staged epilogue
+    // (full 512-B / 1-KiB row stores), except the fp32 residual epilogue,
+    // which is faster from the registers (0.236 vs 0.254 ms out-proj, 0.576
+    // vs 0.598 ms c_proj at ViT-L/14 bs=256); 256 / 257 select SCHED 0 / 1
+    if (variant == 0 || variant == 258)
+      variant = std::is_same_v<Epi, EpiResidual> ? 260 : 258;
     if (variant == 260)
       hipLaunchKernelGGL((gemm256_kernel<T, Epi, 2, true>), dim3(tiles256), dim3(512), 0, s,
                          (const T*)A, (const T*)W, M, N, K, epi, gm);
