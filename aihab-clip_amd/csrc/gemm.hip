@@ -84,20 +84,28 @@ struct EpiStore {
   MICLIP_DEV float4 bias4(int col) const { return ld_bias4(bias, col); }
   MICLIP_DEV float4 bias4nb(int col) const { return ld_bias4_nb(bias, col); }
   MICLIP_DEV float bias1(int col) const { return bias ? bias[col] : 0.f; }
+  // The fp32 result is pinned in a register before the conversion: otherwise
+  // hipcc may fuse the last multiply (or add) with the conversion into one
+  // v_fma_mix* (a single rounding) in some call sites and not in others, and
+  // the tile and tail paths would differ in the last bit.
+  MICLIP_DEV static float fin(float y) {
+    asm volatile("" : "+v"(y));
+    return y;
+  }
   template <bool ASM = false>
   MICLIP_DEV void put4(int r, int c, float4 v, float4 b) const {
     i16x4 o;
-    o[0] = to_bits<T>(act_fn<ACT>(v.x + b.x));
-    o[1] = to_bits<T>(act_fn<ACT>(v.y + b.y));
-    o[2] = to_bits<T>(act_fn<ACT>(v.z + b.z));
-    o[3] = to_bits<T>(act_fn<ACT>(v.w + b.w));
+    o[0] = to_bits<T>(fin(act_fn<ACT>(v.x + b.x)));
+    o[1] = to_bits<T>(fin(act_fn<ACT>(v.y + b.y)));
+    o[2] = to_bits<T>(fin(act_fn<ACT>(v.z + b.z)));
+    o[3] = to_bits<T>(fin(act_fn<ACT>(v.w + b.w)));
     if constexpr (ASM)
       st_b64_asm(C + (size_t)r * ldc + c, o);
     else
       *(i16x4*)(C + (size_t)r * ldc + c) = o;
   }
   MICLIP_DEV void put1(int r, int c, float v, float b) const {
-    C[(size_t)r * ldc + c] = to_t<T>(act_fn<ACT>(v + b));
+    C[(size_t)r * ldc + c] = to_t<T>(fin(act_fn<ACT>(v + b)));
   }
 };
 
@@ -447,23 +455,148 @@ MICLIP_DEV void epilogue_regs(const f32x4 (&acc)[2][2][4][2], const float4 (&bv)
     epilogue_regs_body<true>(acc, bv, m0, n0, wr, wc, lane, M, epi);
 }
 
+// ---------------------------------------------------------------------------
+// Tail of a 256x256 launch. M = 257 * images is never a multiple of 256 rows,
+// so ceil(M/256) * N/256 tiles always leave a last round of a few tiles on a
+// 256-CU chip (1028 tiles = 4 rounds + 4 tiles at N = 1024: the fifth round
+// costs a whole tile time for 0.4 % of the work). The launch therefore
+// covers only `ntm_dp` tile-rows (a whole number of rounds) with 256x256
+// tiles, and the remaining <= 256 rows with extra workgroups that take this
+// path: one 16-row x 64-column task per workgroup over the full K, a skinny
+// GEMM streamed through LDS. Per K-tile (64 k) the A piece (16 rows, 2 KiB)
+// and the W piece (64 columns, 8 KiB) are LDS-DMA'd into one of TS stages
+// (every wave issues one W piece, waves 0-1 one A piece each; same 16-B chunk
+// XOR swizzle as the tiles), TS-1 K-tiles in flight, one counted vmcnt and
+// one barrier per K-tile; waves 0-3 each multiply the A fragments by the B
+// fragments of 16 columns. Every output element accumulates the same
+// v_mfma_f32_16x16x32 chain in the same k order as in the 256x256 tile (k
+// chunks of 32 ascending, lane k-offset 8*(lane>>4)) and the epilogue applies
+// the same functor, so results are bit-identical to an all-tile launch (the
+// encode stays batch-invariant).
+// ---------------------------------------------------------------------------
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the count is an immediate)
+MICLIP_DEV void wait_vmcnt(int n) {
+  switch (n) {
+#define MICLIP_VMC(k) \
+  case k:           \
+    asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    MICLIP_VMC(0) MICLIP_VMC(1) MICLIP_VMC(2) MICLIP_VMC(3) MICLIP_VMC(4) MICLIP_VMC(5)
+    MICLIP_VMC(6) MICLIP_VMC(7) MICLIP_VMC(8) MICLIP_VMC(9) MICLIP_VMC(10) MICLIP_VMC(11)
+    MICLIP_VMC(12) MICLIP_VMC(13) MICLIP_VMC(14) MICLIP_VMC(15) MICLIP_VMC(16)
+#undef MICLIP_VMC
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// RG row groups of 16 x TN columns per workgroup: RG = 1, TN = 64 (waves 0-3
+// own 16 columns each) or RG = 2, TN = 128 (wave = row group x 32 columns).
+template <int RG, int TN>
+struct TailShape {
+  static constexpr int SA = RG * 2048, SB = TN * 128, STG = SA + SB;
+  static constexpr int TS = 122880 / STG < 8 ? 122880 / STG : 8;   // stages (<= 120 KiB)
+  static constexpr int NA = RG * 2, NB = TN / 8;                   // A / W pieces (1 KiB)
+  static constexpr int CPW = RG == 1 ? 16 : 32;                    // columns per wave
+};
+
+template <typename T, class Epi, int RG, int TN>
+MICLIP_DEV void gemm_tail_wg(const T* __restrict__ A, const T* __restrict__ W, int M, int N,
+                             int K, const Epi& epi, int m_start, int task, char* smem) {
+  using S = TailShape<RG, TN>;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ncg = N / TN, rg = task / ncg;
+  const int row0 = m_start + rg * 16 * RG, col0 = (task - rg * ncg) * TN;
+  if (row0 >= M) return;   // whole workgroup (task is workgroup-uniform)
+  const int nk = K / 64;
+  // LDS-DMA pieces of 8 rows x 128 B: A pieces 0..NA-1 by waves 0..NA-1,
+  // W pieces wave, wave+8, ... (NB / 8 per wave)
+  const int lchunk = (lane & 7) ^ (lane >> 3);
+  int ar = row0 + wave * 8 + (lane >> 3);
+  ar = ar < M ? ar : M - 1;
+  const T* asrc = A + (size_t)ar * K + lchunk * 8;
+  const T* bsrc = W + (size_t)(col0 + wave * 8 + (lane >> 3)) * K + lchunk * 8;
+  constexpr int BPW = S::NB / 8;
+  const int per_stage = BPW + (wave < S::NA ? 1 : 0);   // LDS-DMA instructions per stage
+  auto stage = [&](int t) {
+    char* st = smem + (t % S::TS) * S::STG;
+    if (wave < S::NA) glds16(asrc + t * 64, st + wave * 1024);
+#pragma unroll
+    for (int i = 0; i < BPW; ++i)
+      glds16(bsrc + (size_t)i * 64 * K + t * 64, st + S::SA + (wave + 8 * i) * 1024);
+  };
+  const int fr = lane & 15, fk = lane >> 4;
+  const int sw0 = ((0 + fk) ^ (fr & 7)) << 4, sw1 = ((4 + fk) ^ (fr & 7)) << 4;
+  const int wrow = RG == 1 ? 0 : wave >> 2;           // this wave's row group
+  const int wcol = (RG == 1 ? wave : wave & 3) * S::CPW;
+  const bool active = RG == 2 || wave < 4;
+  constexpr int NJ = S::CPW / 16;
+  f32x4 acc[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < S::TS - 1 && t < nk; ++t) stage(t);
+  for (int t = 0; t < nk; ++t) {
+    // retire stage t: the younger loads are stages t+1 .. min(t+TS-2, nk-1)
+    const int younger = nk - 1 - t < S::TS - 2 ? nk - 1 - t : S::TS - 2;
+    wait_vmcnt(younger * per_stage);
+    lds_barrier();
+    // refill the stage read in iteration t-1 (every wave passed this barrier)
+    if (t + S::TS - 1 < nk) stage(t + S::TS - 1);
+    if (active) {
+      const char* st = smem + (t % S::TS) * S::STG;
+      const char* sa = st + (wrow * 16 + fr) * 128;
+      const i16x8 a0 = *(const i16x8*)(sa + sw0);
+      const i16x8 a1 = *(const i16x8*)(sa + sw1);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const char* sb = st + S::SA + (wcol + j * 16 + fr) * 128;
+        acc[j] = Mfma<T>::m16(a0, *(const i16x8*)(sb + sw0), acc[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const char* sb = st + S::SA + (wcol + j * 16 + fr) * 128;
+        acc[j] = Mfma<T>::m16(a1, *(const i16x8*)(sb + sw1), acc[j]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  if (!active) return;
+  // same register epilogue as the tiles: quad transpose -> 4 consecutive columns
+  const int q = (lane & 15) >> 2, jj = lane & 3;
+  const int row = row0 + wrow * 16 + fk * 4 + jj;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int col = col0 + wcol + j * 16 + 4 * q;
+    const float4 v = quad_transpose(acc[j], lane);
+    if (row < M) epi.put4(row, col, v, epi.bias4(col));
+  }
+}
+
+// ntm_dp: tile-rows covered by 256x256 tiles (blocks [0, ntm_dp*ntn)); blocks
+// beyond them run the tail path over rows [ntm_dp*256, M) (see gemm_tail_wg).
 template <typename T, class Epi, int SCHED, bool REGEPI = false>
 __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
                                                       const T* __restrict__ W, int M, int N,
-                                                      int K, Epi epi, int gm) {
+                                                      int K, Epi epi, int gm, int ntm_dp,
+                                                      int tail_wide) {
   constexpr int HALF = 128 * 128;  // bytes of one half-tile slot
   constexpr int EPI_LD = 260;      // fp32 row stride of the epilogue staging (pad 4)
   constexpr int SMEM = 128 * EPI_LD * 4 > 8 * HALF ? 128 * EPI_LD * 4 : 8 * HALF;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
+  const int ntn = N / 256, ntm = ntm_dp;
+  if ((int)blockIdx.x >= ntm * ntn) {
+    if (tail_wide)
+      gemm_tail_wg<T, Epi, 2, 128>(A, W, M, N, K, epi, ntm * 256, blockIdx.x - ntm * ntn, smem);
+    else
+      gemm_tail_wg<T, Epi, 1, 64>(A, W, M, N, K, epi, ntm * 256, blockIdx.x - ntm * ntn, smem);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
-  const int ntn = N / 256, ntm = (M + 255) / 256;
   int tm, tn;
   group_tile(xcd_remap(blockIdx.x, ntm * ntn), ntm, ntn, gm, tm, tn);
   const int m0 = tm * 256, n0 = tn * 256;
-
   // LDS-DMA sources: slot row sr = piece*8 + (lane>>3), piece = wave*2 + pp
   const int lchunk = (lane & 7) ^ (lane >> 3);
   const T* asrc[2][2];
@@ -487,7 +620,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
     glds16(src[0] + k0, dst);
     glds16(src[1] + k0, dst + 1024);
   };
-
   const int fr = lane & 15, fk = lane >> 4;
   // byte offsets inside a slot for k-step s (swizzled 16-B chunk), per fragment row
   const int aoff = (wr * 64 + fr) * 128, boff = (wc * 32 + fr) * 128;
@@ -1073,6 +1205,56 @@ int gemm_group() {
   return g;
 }
 
+int cu_count() {
+  static int ncu = [] {
+    int d = 0, n = 0;
+    if (hipGetDevice(&d) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  return ncu;
+}
+
+// MICLIP_GEMM_TAIL=0 disables the tail split (every row in 256x256 tiles);
+// a variant with kGemmNoTail set does the same for one call (A/B benches).
+constexpr int kGemmNoTail = 1 << 16;
+bool gemm_tail_enabled() {
+  static bool on = [] {
+    const char* e = getenv("MICLIP_GEMM_TAIL");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
+// Split of a 256x256 launch into whole rounds of tiles plus a row tail
+// (gemm_tail_wg). The tile-rows kept in tiles are the largest multiple of
+// ncu / gcd(ntn, ncu) -- the tile count is then a whole number of rounds --
+// provided at most 256 rows are left over; otherwise every row stays in tiles.
+struct TailPlan {
+  int ntm_dp, wgs, wide;
+};
+
+
+TailPlan plan_tail(int M, int N) {
+  const int ntm = (M + 255) / 256, ntn = N / 256, ncu = cu_count();
+  int a = ntn, b = ncu;
+  while (b) {
+    const int t = a % b;
+    a = b;
+    b = t;
+  }
+  const int step = ncu / a;
+  const int ntm_dp = ntm / step * step;
+  const int rows = M - ntm_dp * 256;
+  if (ntm_dp == 0 || rows <= 0 || rows > 256 || N % 64) return TailPlan{ntm, 0, 0};
+  // gemm_tail_wg tasks: 32 x 128 when that still gives >= ncu/2 workgroups
+  // (less W re-read per row), else 16 x 64
+  const int wide_tasks = (rows + 31) / 32 * (N / 128);
+  if (N % 128 == 0 && 2 * wide_tasks >= ncu) return TailPlan{ntm_dp, wide_tasks, 1};
+  return TailPlan{ntm_dp, (rows + 15) / 16 * (N / 64), 0};
+}
+
 bool gemm_shape_ok(int M, int N, int K) {
   return M >= 1 && N >= 128 && K >= BK && N % 128 == 0 && K % BK == 0;
 }
@@ -1081,6 +1263,8 @@ template <typename T, class Epi>
 hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hipStream_t s,
                   int variant = 0) {
   if (!gemm_shape_ok(M, N, K)) return hipErrorInvalidValue;
+  const bool notail = (variant & kGemmNoTail) || !gemm_tail_enabled();
+  variant &= ~kGemmNoTail;
   const int gm = variant >= 1000 ? variant / 1000 : gemm_group();
   variant %= 1000;
   if (variant == 0) variant = gemm_variant();
@@ -1088,13 +1272,7 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
       variant != 260 && variant != 2 && variant != 3)
     return hipErrorInvalidValue;
   if (variant == 3) {   // persistent 256x256
-    static int ncu = [] {
-      int d = 0, n = 0;
-      if (hipGetDevice(&d) != hipSuccess ||
-          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
-        n = 256;
-      return n;
-    }();
+    const int ncu = cu_count();
     const int tiles = ((M + 255) / 256) * (N / 256);
     // needs >= 2 K-tiles (the stream stages at most one tile ahead); the
     // patch-embed epilogue keeps the one-tile-per-workgroup kernel
@@ -1121,18 +1299,20 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
     // vs 0.598 ms c_proj at ViT-L/14 bs=256); 256 / 257 select SCHED 0 / 1
     if (variant == 0 || variant == 258)
       variant = std::is_same_v<Epi, EpiResidual> ? 260 : 258;
+    const TailPlan tp = notail ? TailPlan{(M + 255) / 256, 0, 0} : plan_tail(M, N);
+    const dim3 grid(tp.ntm_dp * (N / 256) + tp.wgs);
     if (variant == 260)
-      hipLaunchKernelGGL((gemm256_kernel<T, Epi, 2, true>), dim3(tiles256), dim3(512), 0, s,
-                         (const T*)A, (const T*)W, M, N, K, epi, gm);
+      hipLaunchKernelGGL((gemm256_kernel<T, Epi, 2, true>), grid, dim3(512), 0, s, (const T*)A,
+                         (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wide);
     else if (variant == 257)
-      hipLaunchKernelGGL((gemm256_kernel<T, Epi, 1>), dim3(tiles256), dim3(512), 0, s,
-                         (const T*)A, (const T*)W, M, N, K, epi, gm);
+      hipLaunchKernelGGL((gemm256_kernel<T, Epi, 1>), grid, dim3(512), 0, s, (const T*)A,
+                         (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wide);
     else if (variant == 256)
-      hipLaunchKernelGGL((gemm256_kernel<T, Epi, 0>), dim3(tiles256), dim3(512), 0, s,
-                         (const T*)A, (const T*)W, M, N, K, epi, gm);
+      hipLaunchKernelGGL((gemm256_kernel<T, Epi, 0>), grid, dim3(512), 0, s, (const T*)A,
+                         (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wide);
     else
-      hipLaunchKernelGGL((gemm256_kernel<T, Epi, 2>), dim3(tiles256), dim3(512), 0, s,
-                         (const T*)A, (const T*)W, M, N, K, epi, gm);
+      hipLaunchKernelGGL((gemm256_kernel<T, Epi, 2>), grid, dim3(512), 0, s, (const T*)A,
+                         (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wide);
     return hipGetLastError();
   }
   constexpr int BM = 128, BN = 128;

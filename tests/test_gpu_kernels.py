@@ -71,6 +71,49 @@ def test_gemm(lib, dt, M, N, K, variant, epi, act):
     assert err <= tol, f"max|err| {err} > {tol}"
 
 
+NO_TAIL = 1 << 16   # gemm.hip kGemmNoTail: every row in 256x256 tiles
+
+
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+@pytest.mark.parametrize("M,N,K", [(16448, 1024, 1024), (16421, 1024, 256), (4112, 4096, 512),
+                                   (16448, 3072, 256), (16500, 1024, 2048), (4352, 4096, 512),
+                                   (4296, 4096, 256), (16640, 3072, 256)])
+@pytest.mark.parametrize("variant", [258, 260, 256])
+@pytest.mark.parametrize("epi,act", [(0, 0), (0, 1), (1, 0), (2, 0)])
+def test_gemm_tail_bitexact(lib, dt, M, N, K, variant, epi, act):
+    """Row tail of a 256x256 launch (rows past the last whole round of tiles,
+    computed as 16-row slivers of tiles (SCHED 2) or by tail workgroups) equals the all-tile launch bit for bit
+    and the fp32 reference within the GEMM tolerance."""
+    code, tdt = DT[dt]
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + epi + act)
+    A = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(tdt)
+    W = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).to(tdt)
+    bias = torch.randn(N, device="cuda", generator=g) * 0.1
+    if epi == 0:
+        mk = lambda: torch.empty(M, N, device="cuda", dtype=tdt)  # noqa: E731
+    elif epi == 1:
+        X0 = torch.randn(M, N, device="cuda", generator=g)
+        mk = X0.clone
+    else:
+        mk = lambda: torch.empty(M, N, device="cuda", dtype=torch.float32)  # noqa: E731
+    outs = []
+    for v in (variant, variant | NO_TAIL):
+        C = mk()
+        _check(lib, lib.miclip_op_gemm(code, A.data_ptr(), W.data_ptr(), bias.data_ptr(), C.data_ptr(),
+                                       M, N, K, epi, act, v, _stream()))
+        outs.append(C)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]), "tail rows differ from the all-tile launch"
+    ref = A[-300:].float() @ W.float().t() + bias
+    if epi == 0 and act == 1:
+        ref = ref * torch.sigmoid(1.702 * ref)
+    if epi == 1:
+        ref = X0[-300:] + ref
+    err = (outs[0][-300:].float() - ref).abs().max().item()
+    tol = (2e-2 if dt == "bf16" else 4e-3) * max(1.0, ref.abs().max().item()) if epi == 0 else 2e-4 * K ** 0.5
+    assert err <= tol, f"max|err| {err} > {tol}"
+
+
 def test_gemm_rejects_bad_shapes(lib):
     A = torch.zeros(16, 64, device="cuda", dtype=torch.float16)
     W = torch.zeros(100, 64, device="cuda", dtype=torch.float16)
