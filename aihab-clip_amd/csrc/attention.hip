@@ -34,31 +34,53 @@ constexpr float kLog2e = 1.4426950408889634f;
 
 // One wave: 32 queries [32*chunk, +32) of one (image, head) against all keys
 // staged in LDS (kimg / vimg). qf: this wave's Q^T fragments (B operand).
+// Leaves the unnormalised O^T (o0: d 0..31, o1: d 32..63) and the row sum
+// of this lane's query; attend_store writes the normalised rows.
+// kt0 / kt_end: key-tile range (kt_end < 0: all tiles the chunk attends to);
+// m: the running max (scaled log2 domain) that lsum and O^T are relative to.
 template <typename T, bool CAUSAL>
 MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg, const i16x8 (&qf)[4], int chunk,
-                             int N, int Npad, float c2, T* op_row0, int D, int lane) {
+                             int N, int Npad, float c2, int lane, f32x16& o0, f32x16& o1,
+                             float& lsum, float& m, int kt0 = 0, int kt_end = -1) {
   const int l32 = lane & 31, hh = lane >> 5;
   const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
   const int q = chunk * 32 + l32;
-  float m = -1e30f, lsum = 0.f;
-  f32x16 o0, o1;
+  m = -1e30f;
+  lsum = 0.f;
 #pragma unroll
   for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; }
   const int nkt_all = Npad >> 5;
-  const int nkt = CAUSAL ? (chunk + 1 < nkt_all ? chunk + 1 : nkt_all) : nkt_all;
-  for (int kt = 0; kt < nkt; ++kt) {
-    // ---- S^T[key][q] = K . Q^T ----
-    f32x16 sacc;
+  const int nkt = kt_end >= 0 ? kt_end
+                              : (CAUSAL ? (chunk + 1 < nkt_all ? chunk + 1 : nkt_all) : nkt_all);
+  // Per-lane LDS byte offsets inside one 32-key tile (4 KiB of K, 4 KiB of V),
+  // loop-invariant: the swizzles depend on the key row only through bits that
+  // a multiple of 32 rows does not change. Per tile only the two running
+  // bases move (+4 KiB), so the reads need no per-tile index arithmetic.
+  int koff[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) koff[s] = l32 * 128 + (((2 * s + hh) ^ ((l32 >> 1) & 7)) << 4);
+  int voff[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    const int ch = 4 * dt + 2 * (g & 1) + (tp >> 1);
+    voff[dt] = (4 * (g >> 1) + tq) * 128 + ((ch ^ (tq << 1)) << 4) + 8 * (tp & 1);
+  }
+  // Two-stage tile pipeline (cdna_hip_programming.md T15): the S^T MFMAs of
+  // tile kt+1 are issued before tile kt's softmax, so the matrix pipe works
+  // while this wave's VALU runs the exponentials (and the softmax does not
+  // wait out the S chain's latency).
+  auto qk = [&](int kt, f32x16& sacc) {
+    const char* ktile = kimg + kt * 4096;
 #pragma unroll
     for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
-    const int key = kt * 32 + l32;
-    const char* krow = kimg + key * 128;
-    const int ksw = (key >> 1) & 7;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const i16x8 kf = *(const i16x8*)(krow + (((2 * s + hh) ^ ksw) << 4));
+      const i16x8 kf = *(const i16x8*)(ktile + koff[s]);
       sacc = Mfma<T>::m32(kf, qf[s], sacc);
     }
+  };
+  auto softmax_pv = [&](int kt, f32x16& sacc) {
+    const char* vtile = vimg + kt * 4096;
     // ---- mask (only tiles that need it), online softmax in base 2 ----
     // Scores stay raw; c2 = scale*log2(e) is folded into one FMA per element:
     // p = exp2(s*c2 - m) with m the running max in the scaled domain.
@@ -115,9 +137,8 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg, const i16x8 (&q
     for (int s2 = 0; s2 < 2; ++s2) {
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
-        const int kr = kt * 32 + 16 * s2 + 4 * (g >> 1) + tq;
-        const int ch = 4 * dt + 2 * (g & 1) + (tp >> 1);
-        const char* a0 = vimg + kr * 128 + ((ch ^ (tq << 1)) << 4) + 8 * (tp & 1);
+        // key rows 16*s2 + 4*(g>>1) + tq (+8) of this tile
+        const char* a0 = vtile + voff[dt] + 16 * 128 * s2;
         const i16x4 lo = ds_read_tr16_b64(a0);
         const i16x4 hi = ds_read_tr16_b64(a0 + 8 * 128);  // rows +8 keep (row & 3)
         const i16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -127,8 +148,25 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg, const i16x8 (&q
           o1 = Mfma<T>::m32(vf, pf[s2], o1);
       }
     }
+  };
+  f32x16 sa, sb;
+  int kt = kt0;
+  if (kt < nkt) qk(kt, sa);
+  for (; kt + 2 <= nkt; kt += 2) {
+    qk(kt + 1, sb);
+    softmax_pv(kt, sa);
+    if (kt + 2 < nkt) qk(kt + 2, sa);
+    softmax_pv(kt + 1, sb);
   }
+  if (kt < nkt) softmax_pv(kt, sa);
   lsum += __shfl_xor(lsum, 32, 64);
+}
+
+template <typename T>
+MICLIP_DEV void attend_store(const f32x16& o0, const f32x16& o1, float lsum, int chunk, int N,
+                             T* op_row0, int D, int lane) {
+  const int hh = lane >> 5;
+  const int q = chunk * 32 + (lane & 31);
   const float inv = 1.0f / lsum;
   if (q < N) {
     T* op = op_row0 + (size_t)q * D;
@@ -146,21 +184,22 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg, const i16x8 (&q
   }
 }
 
+// Padding queries (q >= N) load row N-1: a query only ever meets its own
+// S^T column, P^T column and O^T column, and padding rows are never stored,
+// so finite duplicate data is as good as zeros -- and the load stays
+// branch-free (a zeroing else-branch makes hipcc wait vmcnt(0) for the
+// registers' previous loads at every head, draining the K/V DMA).
 template <typename T>
 MICLIP_DEV void load_q(i16x8 (&qf)[4], const T* base, int ld, int chunk, int N, int lane) {
-  const int q = chunk * 32 + (lane & 31);
-  if (q < N) {
-    const T* qp = base + (size_t)q * ld + 8 * (lane >> 5);
+  int q = chunk * 32 + (lane & 31);
+  q = q < N ? q : N - 1;
+  const T* qp = base + (size_t)q * ld + 8 * (lane >> 5);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = *(const i16x8*)(qp + 16 * s);
-  } else {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = i16x8{0, 0, 0, 0, 0, 0, 0, 0};
-  }
+  for (int s = 0; s < 4; ++s) qf[s] = *(const i16x8*)(qp + 16 * s);
 }
 
 template <typename T, bool CAUSAL>
-__global__ __launch_bounds__(1024) void attention_kernel(const T* __restrict__ qkv,
+__global__ __launch_bounds__(640) void attention_kernel(const T* __restrict__ qkv,
                                                          T* __restrict__ out, int N, int H,
                                                          int Npad, int nchunks, float qk_scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -189,33 +228,48 @@ __global__ __launch_bounds__(1024) void attention_kernel(const T* __restrict__ q
   for (int chunk = wave; chunk < nchunks; chunk += nw) {
     i16x8 qf[4];
     load_q<T>(qf, base, ld, chunk, N, lane);
-    attend_chunk<T, CAUSAL>(kimg, vimg, qf, chunk, N, Npad, c2,
-                            out + (size_t)b * N * D + h * 64, D, lane);
+    f32x16 o0, o1;
+    float lsum, m;
+    attend_chunk<T, CAUSAL>(kimg, vimg, qf, chunk, N, Npad, c2, lane, o0, o1, lsum, m);
+    attend_store<T>(o0, o1, lsum, chunk, N, out + (size_t)b * N * D + h * 64, D, lane);
   }
 }
 
 // ---------------------------------------------------------------------------
-// Pipelined form: one workgroup of nchunks waves (wave w owns query chunk w,
-// N <= 320 -> at most 10 waves) walks hpw consecutive (image, head) pairs.
+// Pipelined form: one workgroup walks hpw consecutive (image, head) pairs.
 // While head j is computed, head j+1's K and V are LDS-DMA'd
 // (global_load_lds_dwordx4 issued from inline asm, 1-KiB pieces of 8 rows,
 // the K/V swizzles applied to the SOURCE address) into the other LDS buffer
 // and each wave's Q fragments for head j+1 are loaded into registers, so the
 // K/V/Q fetch of the next head runs under this head's MFMA + softmax work.
 // One barrier per head: at its top every wave has retired its own DMA and Q
-// loads (s_waitcnt vmcnt(0)) and finished reading the buffer that the next
-// DMA overwrites.
+// loads and finished reading the buffer that the next DMA overwrites.
+//
+// Waves: one per full 32-query chunk. When the last chunk holds only 1-2
+// valid queries (`split`; N = 257 = 8*32 + 1: the CLS token row), a ninth
+// wave doing a whole chunk's work would put 3 waves on one SIMD and 2 on the
+// others. Instead each of the 8 waves, after its own chunk, also takes a
+// contiguous range of that chunk's key tiles (nchunks tiles over nw waves),
+// leaves a partial (o, m, l) per valid query in LDS, and wave 0 merges the
+// partials after the next barrier (flash-decoding style; the same softmax
+// arithmetic up to the fp32 order of the merge).
 // ---------------------------------------------------------------------------
-template <typename T, bool CAUSAL>
-__global__ __launch_bounds__(640) void attention_pipe_kernel(const T* __restrict__ qkv,
-                                                             T* __restrict__ out, int B, int N,
-                                                             int H, int Npad, int hpw,
-                                                             float qk_scale) {
+template <typename T, bool CAUSAL, bool SPLIT>
+__global__ __launch_bounds__(SPLIT ? 512 : 640) void attention_pipe_kernel(
+    const T* __restrict__ qkv, T* __restrict__ out, int B, int N, int H, int Npad, int hpw,
+    float qk_scale) {
+  constexpr bool split = SPLIT;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int img_bytes = Npad * 128;            // one K or V image
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nw = blockDim.x >> 6;              // == nchunks
+  const int nw = blockDim.x >> 6;              // nchunks, or nchunks - 1 when split
+  const int nchunks = Npad >> 5;
+  const int last = nchunks - 1;                // the split chunk
+  const int nvalid = N - 32 * last;            // its valid queries
+  // this wave's key-tile range of the split chunk
+  const int xkt0 = wave * nchunks / nw, xkt1 = (wave + 1) * nchunks / nw;
+  float* part = (float*)(smem + 4 * img_bytes);   // [2][nw][nvalid][66]
   const int D = H * 64, ld = 3 * D;
   const float c2 = qk_scale * kLog2e;
   const int bh0 = blockIdx.x * hpw;
@@ -241,39 +295,113 @@ __global__ __launch_bounds__(640) void attention_pipe_kernel(const T* __restrict
                     (isv ? vimg : kimg) + piece * 1024);
     }
   };
+  // wave 0: merge head bh's partials (LDS parity par) into its output rows
+  auto merge = [&](int bh, int par) {
+    const int b = bh / H, h = bh - b * H;
+    for (int c = 0; c < nvalid; ++c) {
+      const float* pc = part + ((size_t)(par * nw) * nvalid + c) * 66;
+      float mx = -1e30f;
+      for (int i = 0; i < nw; ++i) mx = fmaxf(mx, pc[(size_t)i * nvalid * 66 + 64]);
+      float l = 0.f, o = 0.f;
+      for (int i = 0; i < nw; ++i) {
+        const float* pi = pc + (size_t)i * nvalid * 66;
+        const float w = __builtin_amdgcn_exp2f(pi[64] - mx);
+        l += w * pi[65];
+        o += w * pi[lane];
+      }
+      out[((size_t)b * N + 32 * last + c) * D + h * 64 + lane] = to_t<T>(o / l);
+    }
+  };
 
-  i16x8 qf[4], qn[4];
+  i16x8 qf[4], qn[4], qx[4], qxn[4];
   stage(bh0, 0);
   load_q<T>(qf, head_base(bh0), ld, wave, N, lane);
+  if (split) load_q<T>(qx, head_base(bh0), ld, last, N, lane);
+  // retire head 0's DMA and Q loads; qf / qx named as outputs so hipcc sees
+  // them defined here (guide §5.7 item 1)
+  asm volatile("s_waitcnt vmcnt(0)"
+               : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]), "+v"(qx[0]), "+v"(qx[1]),
+                 "+v"(qx[2]), "+v"(qx[3])
+               :
+               : "memory");
   for (int j = 0; j < nh; ++j) {
     const int bh = bh0 + j, b = bh / H, h = bh - b * H;
-    // retire this wave's DMA of head j and its Q loads; qf named as outputs so
-    // hipcc sees it defined here (its own wait would be a vmcnt(0) at the
-    // first MFMA, i.e. after the next head's DMA is issued: guide §5.7 item 1)
-    asm volatile("s_waitcnt vmcnt(0)"
-                 : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])
-                 :
-                 : "memory");
+    // every wave retired its DMA of head j (prologue, or the q <- qn copies of
+    // head j-1, below) and its partial writes before this barrier
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (j + 1 < nh) {
       stage(bh + 1, (j + 1) & 1);
       load_q<T>(qn, head_base(bh + 1), ld, wave, N, lane);
+      if (split) load_q<T>(qxn, head_base(bh + 1), ld, last, N, lane);
     }
+    if (split && wave == 0 && j > 0) merge(bh - 1, (j - 1) & 1);
     const char* kimg = smem + (j & 1) * 2 * img_bytes;
-    attend_chunk<T, CAUSAL>(kimg, kimg + img_bytes, qf, wave, N, Npad, c2,
-                            out + (size_t)b * N * D + h * 64, D, lane);
+    f32x16 o0, o1;
+    float lsum, m;
+    attend_chunk<T, CAUSAL>(kimg, kimg + img_bytes, qf, wave, N, Npad, c2, lane, o0, o1, lsum,
+                            m);
+    // Take head j+1's Q BEFORE this head's output stores: hipcc's wait for
+    // the qn loads (which also retires the older DMA of head j+1) then never
+    // waits for the stores, which drain under the next head's work.
+    if (j + 1 < nh) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = qn[s];
+      for (int s = 0; s < 4; ++s) qf[s] = qn[s];
+      asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]));
+    }
+    attend_store<T>(o0, o1, lsum, wave, N, out + (size_t)b * N * D + h * 64, D, lane);
+    if (split) {
+      attend_chunk<T, CAUSAL>(kimg, kimg + img_bytes, qx, last, N, Npad, c2, lane, o0, o1, lsum,
+                              m, xkt0, xkt1);
+      if (j + 1 < nh) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) qx[s] = qxn[s];
+        asm volatile("" : "+v"(qx[0]), "+v"(qx[1]), "+v"(qx[2]), "+v"(qx[3]));
+      }
+      // partial for the valid queries: lane (l32, hh) holds O^T rows
+      // d = (r&3) + 8*(r>>2) + 4*hh (+32 in o1) of query column l32
+      const int l32 = lane & 31, hh = lane >> 5;
+      if (l32 < nvalid) {
+        float* pw = part + ((size_t)((j & 1) * nw + wave) * nvalid + l32) * 66;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int d = (r & 3) + 8 * (r >> 2) + 4 * hh;
+          pw[d] = o0[r];
+          pw[32 + d] = o1[r];
+        }
+        if (hh == 0) {
+          pw[64] = m;
+          pw[65] = lsum;
+        }
+      }
+    }
+  }
+  if (split) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (wave == 0 && nh > 0) merge(bh0 + nh - 1, (nh - 1) & 1);
   }
 }
 
-// MICLIP_ATTN=1 forces the one-head-per-workgroup kernel (A/B comparisons).
+// MICLIP_ATTN=1 forces the one-head-per-workgroup kernel; 4 the pipelined
+// kernel with the last-chunk split (A/B comparisons).
 int attn_variant() {
   static int v = [] {
     const char* e = getenv("MICLIP_ATTN");
     return e ? atoi(e) : 0;
   }();
   return v;
+}
+
+// MICLIP_ATTN_SPLIT=1 (or variant 4) spreads a 1-2-query last chunk over the
+// other waves. Off by default: at N = 257 it measured level with the 9-wave
+// form (0.183 vs 0.181 ms per ViT-L/14 layer at bs=256, same process).
+bool attn_split() {
+  static bool on = [] {
+    const char* e = getenv("MICLIP_ATTN_SPLIT");
+    return e && atoi(e) != 0;
+  }();
+  return on;
 }
 
 template <typename T, bool CAUSAL>
@@ -286,13 +414,15 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, hipStrea
   if (variant == 0) variant = attn_variant();
   // pipelined kernel (default; variant 2): two K/V buffers must fit in LDS
   // (N <= 320). ViT-L/14 layer: 0.19-0.21 ms vs 0.21-0.24 ms one head per WG.
-  if (variant != 1 && 2 * lds <= 160 * 1024) {
-    auto kern = attention_pipe_kernel<T, CAUSAL>;
+  if (variant != 1 && 2 * lds + 2 * 10 * 2 * 66 * 4 <= 160 * 1024) {
     static bool attr_set = false;
     if (!attr_set) {
-      const hipError_t e = hipFuncSetAttribute(
-          (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      if (e != hipSuccess) return e;
+      for (const void* k : {(const void*)attention_pipe_kernel<T, CAUSAL, false>,
+                            (const void*)attention_pipe_kernel<T, CAUSAL, true>}) {
+        const hipError_t e =
+            hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+      }
       attr_set = true;
     }
     // one round of workgroups over the CUs at the occupancy LDS allows
@@ -303,16 +433,26 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, hipStrea
         n = 256;
       return n;
     }();
-    const int per_cu = (int)((160 * 1024) / (2 * lds)) < 1 ? 1 : (int)((160 * 1024) / (2 * lds));
+    // split the last chunk's key tiles over the other waves when it holds 1-2 queries
+    const int nvalid = N - 32 * (nchunks - 1);
+    const bool split = !CAUSAL && nchunks >= 5 && nvalid <= 2 && (variant == 4 || attn_split());
+    const int waves = split ? nchunks - 1 : nchunks;
+    const size_t lds_all = 2 * lds + (split ? (size_t)2 * waves * nvalid * 66 * 4 : 0);
+    const int per_cu = (int)((160 * 1024) / lds_all) < 1 ? 1 : (int)((160 * 1024) / lds_all);
     const int heads = B * H, slots = ncu * per_cu;
     int hpw = (heads + slots - 1) / slots;
     hpw = hpw < 1 ? 1 : hpw;
     const int grid = (heads + hpw - 1) / hpw;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(nchunks * 64), 2 * lds, s, (const T*)qkv,
-                       (T*)out, B, N, H, Npad, hpw, 0.125f);
+    if (split)
+      hipLaunchKernelGGL((attention_pipe_kernel<T, CAUSAL, true>), dim3(grid), dim3(waves * 64),
+                         lds_all, s, (const T*)qkv, (T*)out, B, N, H, Npad, hpw, 0.125f);
+    else
+      hipLaunchKernelGGL((attention_pipe_kernel<T, CAUSAL, false>), dim3(grid), dim3(waves * 64),
+                         lds_all, s, (const T*)qkv, (T*)out, B, N, H, Npad, hpw, 0.125f);
     return hipGetLastError();
   }
-  const int per = (nchunks + 15) / 16;
+  // at most 10 waves (3 per SIMD: the two-stage tile pipeline needs ~165 VGPRs)
+  const int per = (nchunks + 9) / 10;
   const int nw = (nchunks + per - 1) / per;
   auto kern = attention_kernel<T, CAUSAL>;
   static bool attr_set = false;

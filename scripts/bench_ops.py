@@ -93,7 +93,7 @@ def main():
         qkv = (torch.randn(M, 3 * W, device="cuda", generator=g)).to(dt)
         o = torch.empty(M, W, device="cuda", dtype=dt)
 
-        for av in (1, 2, 1, 2):
+        for av in (1, 2, 4, 1, 2, 4):
             def fa():
                 rc = lib.miclip_op_attention(0, qkv.data_ptr(), o.data_ptr(), args.batch, args.tokens, H, 0,
                                              av, s)

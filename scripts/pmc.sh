@@ -24,6 +24,17 @@ if [ "${1:-}" = traffic ]; then
   python3 scripts/traffic.py
   exit $?
 fi
+if [ "${1:-}" = attn ]; then
+  CMD=(python3 scripts/bench_ops.py --ops attention --iters 5)
+  i=0
+  for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
+             "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU" \
+             "FETCH_SIZE" "WRITE_SIZE"; do
+    i=$((i+1))
+    pass "a$i" "$grp" "${CMD[@]}"
+  done
+  exit 0
+fi
 CMD=(python3 scripts/bench_ops.py --ops gemm --only fc,proj --variants 0 --iters 5)
 i=0
 for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \

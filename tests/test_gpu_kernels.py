@@ -155,7 +155,7 @@ def _attn_ref(qkv, B, N, H, causal):
     return o.permute(0, 2, 1, 3).reshape(B * N, H * 64)
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 4])
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
 @pytest.mark.parametrize("B,N,H,causal", [(2, 50, 3, 0), (3, 77, 2, 1), (2, 257, 2, 0),
                                           (1, 577, 2, 0), (2, 197, 1, 0), (1, 32, 1, 1),
