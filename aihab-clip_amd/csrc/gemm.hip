@@ -364,17 +364,14 @@ MICLIP_DEV void load_bias_regs(const Epi& epi, int n0, int wc, int lane, float4 
     for (int j = 0; j < 2; ++j) bv[qj][j] = epi.bias4nb(n0 + wc * 64 + qj * 32 + j * 16 + 4 * q);
 }
 
-MICLIP_DEV f32x4 ld_b128_asm(const void* p) {
-  f32x4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
-
 // Residual epilogue, software-pipelined over the 8 row groups (qi, i): the 4
-// x loads of group k+1 are issued (inline asm) before group k is combined and
-// stored, and every wait is an explicit, exactly counted vmcnt naming the
-// loaded registers -- ops younger than group k's loads are group k-1's 4
-// stores and group k+1's 4 loads.
+// x loads of group k+1 are issued before group k is combined and stored.
+// Compiler-visible loads and stores, so hipcc counts them and emits exact
+// vmcnt waits (it hoists the x loads and spills ~20 VGPRs: this path serves
+// the non-default variants 260 and 3 only). (An inline-asm load with a VGPR destination counts as
+// written at the end of its statement, so hipcc may reuse that register --
+// e.g. for a store address -- before the data lands: an intermittent memory
+// fault. cdna_hip_programming.md §5.7 item 1.)
 template <bool GUARD>
 MICLIP_DEV void epilogue_residual_regs(const f32x4 (&acc)[2][2][4][2],
                                        const float4 (&bv)[2][2], int m0, int n0, int wr,
@@ -391,7 +388,7 @@ MICLIP_DEV void epilogue_residual_regs(const f32x4 (&acc)[2][2][4][2],
   auto issue = [&](f32x4 (&x)[4], int k) {
     const int row = row_of(k);
 #pragma unroll
-    for (int f = 0; f < 4; ++f) x[f] = ld_b128_asm(xptr(row, f >> 1, f & 1));
+    for (int f = 0; f < 4; ++f) x[f] = *(const f32x4*)xptr(row, f >> 1, f & 1);
   };
   issue(xa, 0);
 #pragma unroll
@@ -399,12 +396,6 @@ MICLIP_DEV void epilogue_residual_regs(const f32x4 (&acc)[2][2][4][2],
     f32x4 (&cur)[4] = (k & 1) ? xb : xa;
     f32x4 (&nxt)[4] = (k & 1) ? xa : xb;
     if (k + 1 < 8) issue(nxt, k + 1);
-    if (k == 0)
-      asm volatile("s_waitcnt vmcnt(4)" : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]));
-    else if (k + 1 < 8)
-      asm volatile("s_waitcnt vmcnt(8)" : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]));
-    else
-      asm volatile("s_waitcnt vmcnt(4)" : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]));
     const int qi = k >> 2, i = k & 3;
     const int r_true = m0 + wr * 128 + qi * 64 + i * 16 + fk * 4 + jj;
 #pragma unroll
@@ -413,9 +404,9 @@ MICLIP_DEV void epilogue_residual_regs(const f32x4 (&acc)[2][2][4][2],
       const float4 v = quad_transpose(acc[qi][qj][i][j], lane);
       const float4 b = bv[qj][j];
       const f32x4 x = cur[f];
-      const float4 y = make_float4(x[0] + (v.x + b.x), x[1] + (v.y + b.y), x[2] + (v.z + b.z),
-                                   x[3] + (v.w + b.w));
-      if (!GUARD || r_true < M) st_b128_asm(xptr(r_true, qj, j), y);
+      const f32x4 y = {x[0] + (v.x + b.x), x[1] + (v.y + b.y), x[2] + (v.z + b.z),
+                       x[3] + (v.w + b.w)};
+      if (!GUARD || r_true < M) *(f32x4*)xptr(r_true, qj, j) = y;
     }
   }
 }
@@ -577,25 +568,47 @@ template <typename T, class Epi, int SCHED, bool REGEPI = false>
 __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
                                                       const T* __restrict__ W, int M, int N,
                                                       int K, Epi epi, int gm, int ntm_dp,
-                                                      int tail_wide) {
+                                                      int tail_mode) {
   constexpr int HALF = 128 * 128;  // bytes of one half-tile slot
   constexpr int EPI_LD = 260;      // fp32 row stride of the epilogue staging (pad 4)
   constexpr int SMEM = 128 * EPI_LD * 4 > 8 * HALF ? 128 * EPI_LD * 4 : 8 * HALF;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int ntn = N / 256, ntm = ntm_dp;
-  if ((int)blockIdx.x >= ntm * ntn) {
-    if (tail_wide)
-      gemm_tail_wg<T, Epi, 2, 128>(A, W, M, N, K, epi, ntm * 256, blockIdx.x - ntm * ntn, smem);
+  // Block roles. Plain: tiles [0, ntm*ntn), then the tail workgroups. With
+  // TAIL_FIRST (bit 1 of tail_mode) the tail workgroups are interleaved with
+  // the first tiles, 8 of each per 16 consecutive blocks (one of each per
+  // XCD, so tile d keeps XCD d % 8 for xcd_remap): the CUs that draw tail
+  // work start their tile sequence later, which staggers the rounds so that
+  // one round's epilogue store burst overlaps other CUs' main loops instead of
+  // every CU writing at once.
+  const int ndp = ntm * ntn, bid = blockIdx.x;
+  int dp = bid, tail = -1;
+  if (tail_mode & 2) {
+    const int nt8 = gridDim.x - ndp;   // tail blocks (a multiple of 8)
+    if (bid < 2 * nt8) {
+      const int g = bid >> 4, r = bid & 15;
+      dp = r < 8 ? g * 8 + r : -1;
+      tail = r < 8 ? -1 : g * 8 + r - 8;
+    } else {
+      dp = bid - nt8;
+    }
+  } else if (bid >= ndp) {
+    dp = -1;
+    tail = bid - ndp;
+  }
+  if (dp < 0) {
+    if (tail_mode & 1)
+      gemm_tail_wg<T, Epi, 2, 128>(A, W, M, N, K, epi, ntm * 256, tail, smem);
     else
-      gemm_tail_wg<T, Epi, 1, 64>(A, W, M, N, K, epi, ntm * 256, blockIdx.x - ntm * ntn, smem);
+      gemm_tail_wg<T, Epi, 1, 64>(A, W, M, N, K, epi, ntm * 256, tail, smem);
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   int tm, tn;
-  group_tile(xcd_remap(blockIdx.x, ntm * ntn), ntm, ntn, gm, tm, tn);
+  group_tile(xcd_remap(dp, ndp), ntm, ntn, gm, tm, tn);
   const int m0 = tm * 256, n0 = tn * 256;
   // LDS-DMA sources: slot row sr = piece*8 + (lane>>3), piece = wave*2 + pp
   const int lchunk = (lane & 7) ^ (lane >> 3);
@@ -1219,6 +1232,16 @@ int cu_count() {
 // MICLIP_GEMM_TAIL=0 disables the tail split (every row in 256x256 tiles);
 // a variant with kGemmNoTail set does the same for one call (A/B benches).
 constexpr int kGemmNoTail = 1 << 16;
+// kGemmTailFirst / MICLIP_GEMM_TAIL_FIRST=1: tail workgroups interleaved with
+// the first tiles (gemm256_kernel, block roles)
+constexpr int kGemmTailFirst = 1 << 17;
+bool gemm_tail_first() {
+  static bool on = [] {
+    const char* e = getenv("MICLIP_GEMM_TAIL_FIRST");
+    return e && atoi(e) != 0;
+  }();
+  return on;
+}
 bool gemm_tail_enabled() {
   static bool on = [] {
     const char* e = getenv("MICLIP_GEMM_TAIL");
@@ -1264,7 +1287,8 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
                   int variant = 0) {
   if (!gemm_shape_ok(M, N, K)) return hipErrorInvalidValue;
   const bool notail = (variant & kGemmNoTail) || !gemm_tail_enabled();
-  variant &= ~kGemmNoTail;
+  const bool tail_first = variant & kGemmTailFirst;
+  variant &= ~(kGemmNoTail | kGemmTailFirst);
   const int gm = variant >= 1000 ? variant / 1000 : gemm_group();
   variant %= 1000;
   if (variant == 0) variant = gemm_variant();
@@ -1294,12 +1318,17 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   const int tiles256 = ((M + 255) / 256) * (N / 256);
   if (N % 256 == 0 && variant != 128 && (tiles256 >= 256 || variant >= 256)) {
     // default: the staggered schedule (SCHED 2) with the LDS-staged epilogue
-    // (full 512-B / 1-KiB row stores), except the fp32 residual epilogue,
-    // which is faster from the registers (0.236 vs 0.254 ms out-proj, 0.576
-    // vs 0.598 ms c_proj at ViT-L/14 bs=256); 256 / 257 select SCHED 0 / 1
-    if (variant == 0 || variant == 258)
-      variant = std::is_same_v<Epi, EpiResidual> ? 260 : 258;
-    const TailPlan tp = notail ? TailPlan{(M + 255) / 256, 0, 0} : plan_tail(M, N);
+    // (full 512-B / 1-KiB row stores) for every epilogue; 260 = the register
+    // epilogue, 256 / 257 = SCHED 0 / 1. (The fp32 residual register epilogue
+    // was ~5 % faster with inline-asm x loads, but an asm load's destination
+    // is free for hipcc to reuse before the data lands: it faulted
+    // intermittently, so it is gone.)
+    if (variant == 0) variant = 258;
+    TailPlan tp = notail ? TailPlan{(M + 255) / 256, 0, 0} : plan_tail(M, N);
+    if (tp.wgs && (tail_first || gemm_tail_first())) {
+      tp.wgs = (tp.wgs + 7) / 8 * 8;   // interleaved 8 per 16 blocks
+      tp.wide |= 2;
+    }
     const dim3 grid(tp.ntm_dp * (N / 256) + tp.wgs);
     if (variant == 260)
       hipLaunchKernelGGL((gemm256_kernel<T, Epi, 2, true>), grid, dim3(512), 0, s, (const T*)A,

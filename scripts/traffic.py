@@ -22,14 +22,19 @@ M, N, K = 65792, 4096, 1024
 
 
 def launches(path, counter):
-    vals = []
+    """Per-dispatch values of `counter` for the QuickGELU-epilogue 256x256
+    GEMM launches (EpiStore<T, 1>) of the largest grid in the file (the tile
+    rounds plus the row-tail workgroups of M = 65792)."""
+    rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
             if (r["Counter_Name"] == counter and "gemm256_kernel" in r["Kernel_Name"]
-                    and "EpiStore" in r["Kernel_Name"]
-                    and int(r["Grid_Size"]) == ((M + 255) // 256) * (N // 256) * 512):
-                vals.append(float(r["Counter_Value"]))
-    return vals
+                    and "EpiStore" in r["Kernel_Name"] and "Li1EE" in r["Kernel_Name"]):
+                rows.append((int(r["Grid_Size"]), float(r["Counter_Value"])))
+    if not rows:
+        return []
+    g = max(x[0] for x in rows)
+    return [v for gs, v in rows if gs == g]
 
 
 def main():

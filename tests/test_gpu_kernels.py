@@ -78,7 +78,7 @@ NO_TAIL = 1 << 16   # gemm.hip kGemmNoTail: every row in 256x256 tiles
 @pytest.mark.parametrize("M,N,K", [(16448, 1024, 1024), (16421, 1024, 256), (4112, 4096, 512),
                                    (16448, 3072, 256), (16500, 1024, 2048), (4352, 4096, 512),
                                    (4296, 4096, 256), (16640, 3072, 256)])
-@pytest.mark.parametrize("variant", [258, 260, 256])
+@pytest.mark.parametrize("variant", [258, 260, 256, 258 | (1 << 17), 260 | (1 << 17)])
 @pytest.mark.parametrize("epi,act", [(0, 0), (0, 1), (1, 0), (2, 0)])
 def test_gemm_tail_bitexact(lib, dt, M, N, K, variant, epi, act):
     """Row tail of a 256x256 launch (rows past the last whole round of tiles,
