@@ -604,6 +604,15 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
       gemm_tail_wg<T, Epi, 1, 64>(A, W, M, N, K, epi, ntm * 256, tail, smem);
     return;
   }
+  // Round stagger (tail_mode bits 8..15 = microseconds): half of the first
+  // round's workgroups (every other one per XCD) start late, so the CUs run
+  // their tile sequences offset and one half's epilogue store burst falls in
+  // the other half's main loop instead of every CU writing at once.
+  if ((tail_mode >> 8) && bid < 256 && ((bid >> 3) & 1)) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long ticks = (unsigned long long)(tail_mode >> 8) * 100;   // 100 MHz
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -1235,6 +1244,15 @@ constexpr int kGemmNoTail = 1 << 16;
 // kGemmTailFirst / MICLIP_GEMM_TAIL_FIRST=1: tail workgroups interleaved with
 // the first tiles (gemm256_kernel, block roles)
 constexpr int kGemmTailFirst = 1 << 17;
+// kGemmStagger (8 us) / MICLIP_GEMM_STAGGER=<us>: round stagger, see gemm256_kernel
+constexpr int kGemmStagger = 1 << 18;
+int gemm_stagger_us() {
+  static int us = [] {
+    const char* e = getenv("MICLIP_GEMM_STAGGER");
+    return e ? atoi(e) : 0;
+  }();
+  return us;
+}
 bool gemm_tail_first() {
   static bool on = [] {
     const char* e = getenv("MICLIP_GEMM_TAIL_FIRST");
@@ -1288,7 +1306,8 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   if (!gemm_shape_ok(M, N, K)) return hipErrorInvalidValue;
   const bool notail = (variant & kGemmNoTail) || !gemm_tail_enabled();
   const bool tail_first = variant & kGemmTailFirst;
-  variant &= ~(kGemmNoTail | kGemmTailFirst);
+  const bool stagger = variant & kGemmStagger;
+  variant &= ~(kGemmNoTail | kGemmTailFirst | kGemmStagger);
   const int gm = variant >= 1000 ? variant / 1000 : gemm_group();
   variant %= 1000;
   if (variant == 0) variant = gemm_variant();
@@ -1328,6 +1347,11 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
     if (tp.wgs && (tail_first || gemm_tail_first())) {
       tp.wgs = (tp.wgs + 7) / 8 * 8;   // interleaved 8 per 16 blocks
       tp.wide |= 2;
+    }
+    {
+      const int us = stagger ? 8 : gemm_stagger_us();
+      const int tiles = tp.ntm_dp * (N / 256);
+      if (us > 0 && tiles >= 2 * cu_count()) tp.wide |= (us < 255 ? us : 255) << 8;
     }
     const dim3 grid(tp.ntm_dp * (N / 256) + tp.wgs);
     if (variant == 260)

@@ -64,8 +64,10 @@ def main():
             shapes = [sh for sh in shapes if sh[0] in args.only.split(",")]
         # "258n": variant 258 without the row-tail split (gemm.hip kGemmNoTail)
         # "258f": tail workgroups interleaved with the first tiles (kGemmTailFirst)
-        vlist = [int(x[:-1]) | (1 << 16) if x.endswith("n") else
-                 int(x[:-1]) | (1 << 17) if x.endswith("f") else int(x) for x in args.variants.split(",")]
+        # "258s": round stagger (kGemmStagger)
+        suffix = {"n": 1 << 16, "f": 1 << 17, "s": 1 << 18}
+        vlist = [int(x[:-1]) | suffix[x[-1]] if x[-1] in suffix else int(x)
+                 for x in args.variants.split(",")]
         for v in vlist:
             for name, N, K, epi, act in shapes:
                 C = X if epi == 1 else C16
@@ -77,7 +79,7 @@ def main():
                 ms = timeit(fn, args.iters)
                 fl = 2.0 * M * N * K
                 by = 2.0 * M * K + 2.0 * N * K + {0: 2.0, 1: 8.0, 2: 4.0, 3: 0.0}[epi] * M * N
-                out.append(dict(op=f"gemm_{name}", variant=(f"{v & 0xffff}n" if v & (1 << 16) else f"{v & 0xffff}f" if v & (1 << 17) else v), M=M, N=N, K=K, ms=round(ms, 4),
+                out.append(dict(op=f"gemm_{name}", variant=(f"{v & 0xffff}" + "".join(c for c, b in suffix.items() if v & b) if v >> 16 else v), M=M, N=N, K=K, ms=round(ms, 4),
                                 tflops=round(fl / ms / 1e9, 1), gbs=round(by / ms / 1e6, 1)))
                 print(json.dumps(out[-1]), flush=True)
         if args.torch:   # library reference point: torch -> hipBLASLt, same shapes, no epilogue
