@@ -33,7 +33,7 @@ for step in "${steps[@]}"; do
     ksweep)  run ksweep 300 python scripts/bench_ops.py --variants 0 --ksweep --ops gemm ;;
     prof)    export TMPDIR=/tmp
              run prof 600 rocprofv3 --kernel-trace --stats --output-format csv \
-                 -d "$PWD/gpurun_out/prof" -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+                 -d "$PWD/gpurun_out/prof" -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --splits 1 ;;
     benchq)  run benchq 400 python bench.py --steps 5 --warmup 2 --cpu-seconds 5 ;;
     benchab) run benchab 500 python bench.py --steps 8 --warmup 2 --no-cpu-baseline --ab-splits ;;
     *) echo "unknown step $step"; exit 2 ;;
