@@ -1,4 +1,5 @@
-// Fused multi-head attention (head dim 64) over the packed QKV projection.
+// Fused multi-head attention (head dim 64, or 80 for open_clip ViT-H/14) over
+// the packed QKV projection.
 //
 // Replaces, for one ResidualAttentionBlock, torch's
 //   F.multi_head_attention_forward slow path (q.view(tgt_len, bsz*heads, dh) ->
@@ -21,9 +22,13 @@
 //   * K image XOR-swizzled by (row>>1)&7 (conflict-free ds_read_b128 for the
 //     32x32x16 A fragment), V image by (row&3)<<1 (conflict-free tr reads);
 //     both layouts were checked with an LDS bank model of gfx950's lane groups.
+//   * head dim 80 (HeadGeom<80>): K/V rows padded to 96 dims (192 B); S^T takes
+//     5 k-steps, O^T three 32-dim tiles of which the last is half padding
+//     (zero V columns, never stored).
 #include "common.h"
 #include "kernels.h"
 
+#include <cmath>
 #include <cstdlib>
 
 namespace miclip {
@@ -32,55 +37,79 @@ namespace {
 
 constexpr float kLog2e = 1.4426950408889634f;
 
+// LDS geometry of one (image, head)'s K or V image for head dim DH.
+// DH = 64: 128-B rows of 8 16-B chunks, the swizzles XOR over all 8.
+// DH = 80: rows padded to 96 dims (192 B, 12 chunks); chunks 0-7 swizzle as
+// for 64, chunks 8-11 among themselves (x & 3), so the map stays a bijection
+// per row and the lane-invariant offsets of attend_chunk still hold.
+template <int DH>
+struct HeadGeom {
+  static_assert(DH == 64 || DH == 80, "head dim 64 or 80");
+  static constexpr int NKS = DH / 16;         // k-steps of S^T = K . Q^T (32x32x16)
+  static constexpr int NDT = (DH + 31) / 32;  // 32-dim tiles of O^T
+  static constexpr int ROWB = NDT * 64;       // LDS bytes per key row
+  static constexpr int CH = ROWB / 16;        // 16-B chunks per row
+  static constexpr int TILEB = 32 * ROWB;     // one 32-key tile
+  // physical chunk of logical chunk c under the row's swizzle key x (0..7)
+  static MICLIP_DEV int swz(int c, int x) {
+    return (ROWB == 128 || c < 8) ? (c ^ x) : 8 + ((c - 8) ^ (x & 3));
+  }
+};
+
 // One wave: 32 queries [32*chunk, +32) of one (image, head) against all keys
 // staged in LDS (kimg / vimg). qf: this wave's Q^T fragments (B operand).
-// Leaves the unnormalised O^T (o0: d 0..31, o1: d 32..63) and the row sum
+// Leaves the unnormalised O^T (o[dt]: d 32*dt .. 32*dt+31) and the row sum
 // of this lane's query; attend_store writes the normalised rows.
 // kt0 / kt_end: key-tile range (kt_end < 0: all tiles the chunk attends to);
 // m: the running max (scaled log2 domain) that lsum and O^T are relative to.
-template <typename T, bool CAUSAL>
-MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg, const i16x8 (&qf)[4], int chunk,
-                             int N, int Npad, float c2, int lane, f32x16& o0, f32x16& o1,
-                             float& lsum, float& m, int kt0 = 0, int kt_end = -1) {
+template <typename T, bool CAUSAL, int DH>
+MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
+                             const i16x8 (&qf)[HeadGeom<DH>::NKS], int chunk, int N, int Npad,
+                             float c2, int lane, f32x16 (&o)[HeadGeom<DH>::NDT], float& lsum,
+                             float& m, int kt0 = 0, int kt_end = -1) {
+  using G = HeadGeom<DH>;
   const int l32 = lane & 31, hh = lane >> 5;
   const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
   const int q = chunk * 32 + l32;
   m = -1e30f;
   lsum = 0.f;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) { o0[r] = 0.f; o1[r] = 0.f; }
+  for (int r = 0; r < 16; ++r)
+#pragma unroll
+    for (int dt = 0; dt < G::NDT; ++dt) o[dt][r] = 0.f;
   const int nkt_all = Npad >> 5;
   const int nkt = kt_end >= 0 ? kt_end
                               : (CAUSAL ? (chunk + 1 < nkt_all ? chunk + 1 : nkt_all) : nkt_all);
-  // Per-lane LDS byte offsets inside one 32-key tile (4 KiB of K, 4 KiB of V),
+  // Per-lane LDS byte offsets inside one 32-key tile (TILEB bytes of K, of V),
   // loop-invariant: the swizzles depend on the key row only through bits that
   // a multiple of 32 rows does not change. Per tile only the two running
-  // bases move (+4 KiB), so the reads need no per-tile index arithmetic.
-  int koff[4];
+  // bases move, so the reads need no per-tile index arithmetic.
+  int koff[G::NKS];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) koff[s] = l32 * 128 + (((2 * s + hh) ^ ((l32 >> 1) & 7)) << 4);
-  int voff[2];
+  for (int s = 0; s < G::NKS; ++s)
+    koff[s] = l32 * G::ROWB + (G::swz(2 * s + hh, (l32 >> 1) & 7) << 4);
+  int voff[G::NDT];
 #pragma unroll
-  for (int dt = 0; dt < 2; ++dt) {
+  for (int dt = 0; dt < G::NDT; ++dt) {
     const int ch = 4 * dt + 2 * (g & 1) + (tp >> 1);
-    voff[dt] = (4 * (g >> 1) + tq) * 128 + ((ch ^ (tq << 1)) << 4) + 8 * (tp & 1);
+    voff[dt] = (4 * (g >> 1) + tq) * G::ROWB + (G::swz(ch, tq << 1) << 4) + 8 * (tp & 1);
   }
   // Two-stage tile pipeline (cdna_hip_programming.md T15): the S^T MFMAs of
   // tile kt+1 are issued before tile kt's softmax, so the matrix pipe works
   // while this wave's VALU runs the exponentials (and the softmax does not
   // wait out the S chain's latency).
   auto qk = [&](int kt, f32x16& sacc) {
-    const char* ktile = kimg + kt * 4096;
+    const char* ktile = kimg + kt * G::TILEB;
 #pragma unroll
     for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < G::NKS; ++s) {
       const i16x8 kf = *(const i16x8*)(ktile + koff[s]);
       sacc = Mfma<T>::m32(kf, qf[s], sacc);
     }
   };
   auto softmax_pv = [&](int kt, f32x16& sacc) {
-    const char* vtile = vimg + kt * 4096;
+    const char* vtile = vimg + kt * G::TILEB;
     // ---- mask (only tiles that need it), online softmax in base 2 ----
     // Scores stay raw; c2 = scale*log2(e) is folded into one FMA per element:
     // p = exp2(s*c2 - m) with m the running max in the scaled domain.
@@ -107,7 +136,9 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg, const i16x8 (&q
       m = mnew;
       lsum *= alpha;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+      for (int r = 0; r < 16; ++r)
+#pragma unroll
+        for (int dt = 0; dt < G::NDT; ++dt) o[dt][r] *= alpha;
     }
     // raw v_exp_f32: exp2f's denormal-range fix-up (cmp/cndmask/ldexp per
     // element) is dead weight here -- results below 2^-126 vanish in the fp16
@@ -136,16 +167,13 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg, const i16x8 (&q
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
+      for (int dt = 0; dt < G::NDT; ++dt) {
         // key rows 16*s2 + 4*(g>>1) + tq (+8) of this tile
-        const char* a0 = vtile + voff[dt] + 16 * 128 * s2;
+        const char* a0 = vtile + voff[dt] + 16 * G::ROWB * s2;
         const i16x4 lo = ds_read_tr16_b64(a0);
-        const i16x4 hi = ds_read_tr16_b64(a0 + 8 * 128);  // rows +8 keep (row & 3)
+        const i16x4 hi = ds_read_tr16_b64(a0 + 8 * G::ROWB);  // rows +8 keep (row & 3)
         const i16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        if (dt == 0)
-          o0 = Mfma<T>::m32(vf, pf[s2], o0);
-        else
-          o1 = Mfma<T>::m32(vf, pf[s2], o1);
+        o[dt] = Mfma<T>::m32(vf, pf[s2], o[dt]);
       }
     }
   };
@@ -162,8 +190,8 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg, const i16x8 (&q
   lsum += __shfl_xor(lsum, 32, 64);
 }
 
-template <typename T>
-MICLIP_DEV void attend_store(const f32x16& o0, const f32x16& o1, float lsum, int chunk, int N,
+template <typename T, int DH>
+MICLIP_DEV void attend_store(const f32x16 (&o)[HeadGeom<DH>::NDT], float lsum, int chunk, int N,
                              T* op_row0, int D, int lane) {
   const int hh = lane >> 5;
   const int q = chunk * 32 + (lane & 31);
@@ -171,13 +199,13 @@ MICLIP_DEV void attend_store(const f32x16& o0, const f32x16& o1, float lsum, int
   if (q < N) {
     T* op = op_row0 + (size_t)q * D;
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
+    for (int dt = 0; dt < HeadGeom<DH>::NDT; ++dt) {
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) {
+        if (32 * dt + 8 * rg >= DH) continue;  // padding dims (DH = 80: rg >= 2 of tile 2)
         i16x4 w;
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          w[e] = to_bits<T>((dt == 0 ? o0[4 * rg + e] : o1[4 * rg + e]) * inv);
+        for (int e = 0; e < 4; ++e) w[e] = to_bits<T>(o[dt][4 * rg + e] * inv);
         *(i16x4*)(op + 32 * dt + 8 * rg + 4 * hh) = w;
       }
     }
@@ -189,49 +217,54 @@ MICLIP_DEV void attend_store(const f32x16& o0, const f32x16& o1, float lsum, int
 // so finite duplicate data is as good as zeros -- and the load stays
 // branch-free (a zeroing else-branch makes hipcc wait vmcnt(0) for the
 // registers' previous loads at every head, draining the K/V DMA).
-template <typename T>
-MICLIP_DEV void load_q(i16x8 (&qf)[4], const T* base, int ld, int chunk, int N, int lane) {
+template <typename T, int DH>
+MICLIP_DEV void load_q(i16x8 (&qf)[HeadGeom<DH>::NKS], const T* base, int ld, int chunk, int N,
+                       int lane) {
   int q = chunk * 32 + (lane & 31);
   q = q < N ? q : N - 1;
   const T* qp = base + (size_t)q * ld + 8 * (lane >> 5);
 #pragma unroll
-  for (int s = 0; s < 4; ++s) qf[s] = *(const i16x8*)(qp + 16 * s);
+  for (int s = 0; s < HeadGeom<DH>::NKS; ++s) qf[s] = *(const i16x8*)(qp + 16 * s);
 }
 
-template <typename T, bool CAUSAL>
-__global__ __launch_bounds__(640) void attention_kernel(const T* __restrict__ qkv,
-                                                         T* __restrict__ out, int N, int H,
-                                                         int Npad, int nchunks, float qk_scale) {
+// One workgroup per (image, head). Launch bounds: 10 waves for DH = 64 (3
+// per SIMD, ~165 VGPRs); DH = 80 carries a third O^T tile and a fifth Q
+// fragment, so 8 waves (2 per SIMD, up to 256 VGPRs).
+template <typename T, bool CAUSAL, int DH>
+__global__ __launch_bounds__(DH == 64 ? 640 : 512) void attention_kernel(
+    const T* __restrict__ qkv, T* __restrict__ out, int N, int H, int Npad, int nchunks,
+    float qk_scale) {
+  using G = HeadGeom<DH>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* kimg = smem;               // [Npad][64] T, 128-B rows
-  char* vimg = smem + Npad * 128;  // [Npad][64] T, 128-B rows
+  char* kimg = smem;                  // [Npad][ROWB/2] T
+  char* vimg = smem + Npad * G::ROWB;  // [Npad][ROWB/2] T
 
   const int bh = blockIdx.x;
   const int b = bh / H, h = bh - b * H;
-  const int D = H * 64, ld = 3 * D;
-  const T* base = qkv + (size_t)b * N * ld + h * 64;
+  const int D = H * DH, ld = 3 * D;
+  const T* base = qkv + (size_t)b * N * ld + h * DH;
 
-  for (int idx = threadIdx.x; idx < Npad * 8; idx += blockDim.x) {
-    const int row = idx >> 3, c = idx & 7;
+  for (int idx = threadIdx.x; idx < Npad * G::CH; idx += blockDim.x) {
+    const int row = idx / G::CH, c = idx - row * G::CH;
     i16x8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (row < N) {
+    if (row < N && c * 8 < DH) {
       kv = *(const i16x8*)(base + (size_t)row * ld + D + c * 8);
       vv = *(const i16x8*)(base + (size_t)row * ld + 2 * D + c * 8);
     }
-    *(i16x8*)(kimg + row * 128 + ((c ^ ((row >> 1) & 7)) << 4)) = kv;
-    *(i16x8*)(vimg + row * 128 + ((c ^ ((row & 3) << 1)) << 4)) = vv;
+    *(i16x8*)(kimg + row * G::ROWB + (G::swz(c, (row >> 1) & 7) << 4)) = kv;
+    *(i16x8*)(vimg + row * G::ROWB + (G::swz(c, (row & 3) << 1) << 4)) = vv;
   }
   __syncthreads();
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const float c2 = qk_scale * kLog2e;
   for (int chunk = wave; chunk < nchunks; chunk += nw) {
-    i16x8 qf[4];
-    load_q<T>(qf, base, ld, chunk, N, lane);
-    f32x16 o0, o1;
+    i16x8 qf[G::NKS];
+    load_q<T, DH>(qf, base, ld, chunk, N, lane);
+    f32x16 o[G::NDT];
     float lsum, m;
-    attend_chunk<T, CAUSAL>(kimg, vimg, qf, chunk, N, Npad, c2, lane, o0, o1, lsum, m);
-    attend_store<T>(o0, o1, lsum, chunk, N, out + (size_t)b * N * D + h * 64, D, lane);
+    attend_chunk<T, CAUSAL, DH>(kimg, vimg, qf, chunk, N, Npad, c2, lane, o, lsum, m);
+    attend_store<T, DH>(o, lsum, chunk, N, out + (size_t)b * N * D + h * DH, D, lane);
   }
 }
 
@@ -315,8 +348,8 @@ __global__ __launch_bounds__(SPLIT ? 512 : 640) void attention_pipe_kernel(
 
   i16x8 qf[4], qn[4], qx[4], qxn[4];
   stage(bh0, 0);
-  load_q<T>(qf, head_base(bh0), ld, wave, N, lane);
-  if (split) load_q<T>(qx, head_base(bh0), ld, last, N, lane);
+  load_q<T, 64>(qf, head_base(bh0), ld, wave, N, lane);
+  if (split) load_q<T, 64>(qx, head_base(bh0), ld, last, N, lane);
   // retire head 0's DMA and Q loads; qf / qx named as outputs so hipcc sees
   // them defined here (guide §5.7 item 1)
   asm volatile("s_waitcnt vmcnt(0)"
@@ -332,15 +365,14 @@ __global__ __launch_bounds__(SPLIT ? 512 : 640) void attention_pipe_kernel(
     __builtin_amdgcn_s_barrier();
     if (j + 1 < nh) {
       stage(bh + 1, (j + 1) & 1);
-      load_q<T>(qn, head_base(bh + 1), ld, wave, N, lane);
-      if (split) load_q<T>(qxn, head_base(bh + 1), ld, last, N, lane);
+      load_q<T, 64>(qn, head_base(bh + 1), ld, wave, N, lane);
+      if (split) load_q<T, 64>(qxn, head_base(bh + 1), ld, last, N, lane);
     }
     if (split && wave == 0 && j > 0) merge(bh - 1, (j - 1) & 1);
     const char* kimg = smem + (j & 1) * 2 * img_bytes;
-    f32x16 o0, o1;
+    f32x16 o[2];
     float lsum, m;
-    attend_chunk<T, CAUSAL>(kimg, kimg + img_bytes, qf, wave, N, Npad, c2, lane, o0, o1, lsum,
-                            m);
+    attend_chunk<T, CAUSAL, 64>(kimg, kimg + img_bytes, qf, wave, N, Npad, c2, lane, o, lsum, m);
     // Take head j+1's Q BEFORE this head's output stores: hipcc's wait for
     // the qn loads (which also retires the older DMA of head j+1) then never
     // waits for the stores, which drain under the next head's work.
@@ -349,10 +381,10 @@ __global__ __launch_bounds__(SPLIT ? 512 : 640) void attention_pipe_kernel(
       for (int s = 0; s < 4; ++s) qf[s] = qn[s];
       asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]));
     }
-    attend_store<T>(o0, o1, lsum, wave, N, out + (size_t)b * N * D + h * 64, D, lane);
+    attend_store<T, 64>(o, lsum, wave, N, out + (size_t)b * N * D + h * 64, D, lane);
     if (split) {
-      attend_chunk<T, CAUSAL>(kimg, kimg + img_bytes, qx, last, N, Npad, c2, lane, o0, o1, lsum,
-                              m, xkt0, xkt1);
+      attend_chunk<T, CAUSAL, 64>(kimg, kimg + img_bytes, qx, last, N, Npad, c2, lane, o, lsum, m,
+                                  xkt0, xkt1);
       if (j + 1 < nh) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) qx[s] = qxn[s];
@@ -366,8 +398,8 @@ __global__ __launch_bounds__(SPLIT ? 512 : 640) void attention_pipe_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int d = (r & 3) + 8 * (r >> 2) + 4 * hh;
-          pw[d] = o0[r];
-          pw[32 + d] = o1[r];
+          pw[d] = o[0][r];
+          pw[32 + d] = o[1][r];
         }
         if (hh == 0) {
           pw[64] = m;
@@ -404,9 +436,36 @@ bool attn_split() {
   return on;
 }
 
+// one workgroup per (image, head)
+template <typename T, bool CAUSAL, int DH>
+hipError_t attn_launch_plain(const void* qkv, void* out, int B, int N, int H, hipStream_t s) {
+  using G = HeadGeom<DH>;
+  const int Npad = (N + 31) & ~31;
+  const int nchunks = Npad / 32;
+  const size_t lds = (size_t)Npad * G::ROWB * 2;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  // at most 10 (DH 64) / 8 (DH 80) waves, see attention_kernel's launch bounds
+  constexpr int maxw = DH == 64 ? 10 : 8;
+  const int per = (nchunks + maxw - 1) / maxw;
+  const int nw = (nchunks + per - 1) / per;
+  auto kern = attention_kernel<T, CAUSAL, DH>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute(
+        (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(B * H), dim3(nw * 64), lds, s, (const T*)qkv, (T*)out, N, H,
+                     Npad, nchunks, 1.0f / sqrtf((float)DH));
+  return hipGetLastError();
+}
+
 template <typename T, bool CAUSAL>
-hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, hipStream_t s,
+hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, hipStream_t s,
                        int variant) {
+  if (dh == 80) return attn_launch_plain<T, CAUSAL, 80>(qkv, out, B, N, H, s);
+  if (dh != 64) return hipErrorInvalidValue;
   const int Npad = (N + 31) & ~31;
   const int nchunks = Npad / 32;
   const size_t lds = (size_t)Npad * 256;
@@ -451,32 +510,19 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, hipStrea
                          lds_all, s, (const T*)qkv, (T*)out, B, N, H, Npad, hpw, 0.125f);
     return hipGetLastError();
   }
-  // at most 10 waves (3 per SIMD: the two-stage tile pipeline needs ~165 VGPRs)
-  const int per = (nchunks + 9) / 10;
-  const int nw = (nchunks + per - 1) / per;
-  auto kern = attention_kernel<T, CAUSAL>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute(
-        (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(kern, dim3(B * H), dim3(nw * 64), lds, s, (const T*)qkv, (T*)out, N, H,
-                     Npad, nchunks, 0.125f);
-  return hipGetLastError();
+  return attn_launch_plain<T, CAUSAL, 64>(qkv, out, B, N, H, s);
 }
 
 }  // namespace
 
 hipError_t attention(int dtype, const void* qkv, void* out, int B, int N, int H, int causal,
-                     hipStream_t s, int variant) {
+                     hipStream_t s, int variant, int head_dim) {
   if (B < 1 || N < 1 || H < 1) return hipErrorInvalidValue;
   if (dtype == kF16)
-    return causal ? attn_launch<_Float16, true>(qkv, out, B, N, H, s, variant)
-                  : attn_launch<_Float16, false>(qkv, out, B, N, H, s, variant);
-  return causal ? attn_launch<__bf16, true>(qkv, out, B, N, H, s, variant)
-                : attn_launch<__bf16, false>(qkv, out, B, N, H, s, variant);
+    return causal ? attn_launch<_Float16, true>(qkv, out, B, N, H, head_dim, s, variant)
+                  : attn_launch<_Float16, false>(qkv, out, B, N, H, head_dim, s, variant);
+  return causal ? attn_launch<__bf16, true>(qkv, out, B, N, H, head_dim, s, variant)
+                : attn_launch<__bf16, false>(qkv, out, B, N, H, head_dim, s, variant);
 }
 
 }  // namespace miclip

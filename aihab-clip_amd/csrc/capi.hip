@@ -266,7 +266,7 @@ double gemm_bytes(double M, double N, double K, double c_bytes) {
 }
 
 int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, int W, int H,
-              int causal, hipStream_t s) {
+              int dh, int causal, hipStream_t s) {
   const int M = items * N, dt = m->dtype;
   const double dM = M, dW = W;
   {
@@ -279,8 +279,8 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
   }
   {
     const double n = N;
-    ProfScope p(m, K_ATTENTION, s, 4.0 * items * H * n * n * 64, dM * dW * 2 * 4);
-    MICLIP_HIP(attention(dt, w.qkv, w.o, items, N, H, causal, s));
+    ProfScope p(m, K_ATTENTION, s, 4.0 * items * H * n * n * dh, dM * dW * 2 * 4);
+    MICLIP_HIP(attention(dt, w.qkv, w.o, items, N, H, causal, s, 0, dh));
   }
   {
     ProfScope p(m, K_GEMM_OUT, s, gemm_flops(dM, dW, dW), gemm_bytes(dM, dW, dW, 8));
@@ -333,7 +333,8 @@ int encode_image_part(miclip_model* m, Workspace w, const float* images, int B, 
                       uint32_t flags, hipStream_t s) {
   const auto& c = m->cfg;
   const int P = c.vision_patch_size, R = c.image_resolution, W = c.vision_width;
-  const int g = R / P, np = g * g, N = np + 1, H = W / 64, dt = m->dtype;
+  const int dh = c.vision_head_dim, g = R / P, np = g * g, N = np + 1, H = W / dh;
+  const int dt = m->dtype;
   const int M = B * N;
   int rc;
   {
@@ -351,7 +352,7 @@ int encode_image_part(miclip_model* m, Workspace w, const float* images, int B, 
     MICLIP_HIP(layernorm(dt, w.x, nullptr, 1, m->ln_pre_g, m->ln_pre_b, w.x, nullptr, M, W, 0, s));
   }
   for (int l = 0; l < c.vision_layers; ++l)
-    if ((rc = run_block(m, m->vblocks[l], w, B, N, W, H, 0, s))) return rc;
+    if ((rc = run_block(m, m->vblocks[l], w, B, N, W, H, dh, 0, s))) return rc;
   const bool proj = flags & MICLIP_FLAG_APPLY_PROJ, norm = flags & MICLIP_FLAG_NORMALIZE;
   // ln_post on the CLS rows only (clip/model.py:228): rows b*N
   ProfScope p(m, K_HEAD, s, proj ? 2.0 * B * W * c.embed_dim : 0.0, (double)B * W * 8);
@@ -377,9 +378,14 @@ bool cfg_ok(const miclip_config& c, std::string& why) {
     return bad("transformer_heads * 64 must equal transformer_width (head dim 64)");
   if (c.vision_patch_size < 1 || c.image_resolution % c.vision_patch_size)
     return bad("image_resolution must be a multiple of vision_patch_size");
+  if (c.vision_head_dim != 64 && c.vision_head_dim != 80)
+    return bad("vision_head_dim must be 64 or 80");
+  if (c.vision_width % c.vision_head_dim) return bad("vision_width % vision_head_dim != 0");
   const int g = c.image_resolution / c.vision_patch_size;
-  if ((g * g + 1 + 31) / 32 * 32 * 256 > 160 * 1024)
-    return bad("too many vision tokens for the attention kernel (max 640)");
+  // K and V images of one head in LDS: 128-B rows (dh 64) / 192-B rows (dh 80)
+  const int rowb = c.vision_head_dim == 64 ? 128 : 192;
+  if ((g * g + 1 + 31) / 32 * 32 * 2 * rowb > 160 * 1024)
+    return bad("too many vision tokens for the attention kernel (max 640 at dh 64, 416 at 80)");
   if (c.context_length < 1 || c.context_length > 640) return bad("context_length out of range");
   if (c.vision_layers < 1 || c.transformer_layers < 0) return bad("bad layer count");
   if (c.embed_dim < 1 || c.vocab_size < 1) return bad("bad embed_dim / vocab_size");
@@ -399,13 +405,15 @@ int miclip_abi_version(void) { return MICLIP_ABI_VERSION; }
 int miclip_model_create(const miclip_config* cfg, int device, miclip_model** out) {
   if (!cfg || !out) return fail(MICLIP_EINVAL, "null argument");
   std::string why;
-  if (!cfg_ok(*cfg, why)) return fail(MICLIP_EINVAL, "invalid config: " + why);
+  miclip_config c = *cfg;
+  if (c.vision_head_dim == 0) c.vision_head_dim = 64;  // ABI v2 callers: zero-filled field
+  if (!cfg_ok(c, why)) return fail(MICLIP_EINVAL, "invalid config: " + why);
   int ndev = 0;
   MICLIP_HIP(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return fail(MICLIP_EINVAL, "invalid device index");
   MICLIP_HIP(hipSetDevice(device));
   auto* m = new miclip_model();
-  m->cfg = *cfg;
+  m->cfg = c;
   m->device = device;
   m->dtype = cfg->compute_dtype;
   const int P = cfg->vision_patch_size, Wv = cfg->vision_width, Wt = cfg->transformer_width;
@@ -563,7 +571,7 @@ int miclip_encode_text(miclip_model* m, const int64_t* tokens, int32_t P, float*
     MICLIP_HIP(token_embed(tokens, m->tok_emb, m->tpos, w.x, w.rows, P, L, W, c.vocab_size, s));
   }
   for (int l = 0; l < c.transformer_layers; ++l)
-    if ((rc = run_block(m, m->tblocks[l], w, P, L, W, H, 1, s))) return rc;
+    if ((rc = run_block(m, m->tblocks[l], w, P, L, W, H, 64, 1, s))) return rc;
   float* xb = x_before ? x_before : w.feat;
   ProfScope p(m, K_HEAD, s, x_proj ? 2.0 * P * W * c.embed_dim : 0.0, (double)P * W * 8);
   MICLIP_HIP(layernorm(m->dtype, w.x, w.rows, 0, m->ln_final_g, m->ln_final_b, xb, nullptr, P, W,
@@ -721,9 +729,12 @@ int miclip_op_layernorm(int32_t dtype, const float* in, const float* gamma, cons
 }
 
 int miclip_op_attention(int32_t dtype, const void* qkv, void* out, int32_t B, int32_t N,
-                        int32_t H, int32_t causal, int32_t variant, void* stream) {
+                        int32_t H, int32_t head_dim, int32_t causal, int32_t variant,
+                        void* stream) {
   if (!qkv || !out) return fail(MICLIP_EINVAL, "null argument");
-  MICLIP_HIP(attention(dtype, qkv, out, B, N, H, causal, (hipStream_t)stream, variant));
+  if (head_dim == 0) head_dim = 64;
+  if (head_dim != 64 && head_dim != 80) return fail(MICLIP_EINVAL, "head_dim must be 64 or 80");
+  MICLIP_HIP(attention(dtype, qkv, out, B, N, H, causal, (hipStream_t)stream, variant, head_dim));
   return 0;
 }
 

@@ -40,13 +40,14 @@ hipError_t layernorm(int dtype, const float* in, const int32_t* rows, int in_str
                      int R, int D, int normalize, hipStream_t s);
 
 // ---- fused multi-head attention over a packed QKV buffer ----
-// qkv: [B*N, 3*H*64] compute dtype (torch in_proj order q|k|v); out: [B*N, H*64].
-// head dim 64; causal adds the -inf strictly-upper-triangular mask (clip/model.py:323-329).
-// variant: 0 = default (MICLIP_ATTN env, else the pipelined multi-head kernel
-// when N <= 320, one head per workgroup above), 1 = one head per workgroup,
-// 2 = pipelined.
+// qkv: [B*N, 3*H*dh] compute dtype (torch in_proj order q|k|v); out: [B*N, H*dh].
+// head dim dh = 64 (OpenAI CLIP) or 80 (open_clip ViT-H/14 vision tower; one head
+// per workgroup); causal adds the -inf strictly-upper-triangular mask
+// (clip/model.py:323-329). variant (dh 64): 0 = default (MICLIP_ATTN env, else the
+// pipelined multi-head kernel when N <= 320, one head per workgroup above),
+// 1 = one head per workgroup, 2 = pipelined, 4 = pipelined + last-chunk split.
 hipError_t attention(int dtype, const void* qkv, void* out, int B, int N, int H, int causal,
-                     hipStream_t s, int variant = 0);
+                     hipStream_t s, int variant = 0, int head_dim = 64);
 
 // ---- embeddings / gathers ----
 // images fp32 [B,3,R,R] -> patches [B*g*g, Kp] compute dtype, col = c*P*P + ky*P + kx,

@@ -10,7 +10,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MICLIP_LIB", os.path.join(_HERE, "libmiclip.so"))
 
-ABI_VERSION = 2          # include/miclip.h MICLIP_ABI_VERSION
+ABI_VERSION = 3          # include/miclip.h MICLIP_ABI_VERSION
 MICLIP_FP16 = 0
 MICLIP_BF16 = 1
 MICLIP_ACT_QUICKGELU = 1
@@ -35,7 +35,7 @@ class MiclipConfig(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "embed_dim", "image_resolution", "vision_layers", "vision_width", "vision_patch_size",
         "context_length", "vocab_size", "transformer_width", "transformer_heads",
-        "transformer_layers", "compute_dtype", "act")]
+        "transformer_layers", "compute_dtype", "act", "vision_head_dim")]
 
 
 class MiclipTensor(ctypes.Structure):
@@ -87,7 +87,7 @@ def load_library(path: str = None):
         "miclip_profile_read": ([vp, ctypes.POINTER(MiclipKernelStat), i32, i32], ctypes.c_int),
         "miclip_op_gemm": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp], ctypes.c_int),
         "miclip_op_layernorm": ([i32, vp, vp, vp, vp, i32, i32, i32, vp], ctypes.c_int),
-        "miclip_op_attention": ([i32, vp, vp, i32, i32, i32, i32, i32, vp], ctypes.c_int),
+        "miclip_op_attention": ([i32, vp, vp, i32, i32, i32, i32, i32, i32, vp], ctypes.c_int),
         "miclip_preprocess": ([vp, vp, ctypes.POINTER(MiclipImageDesc), i32, vp, i32, vp],
                               ctypes.c_int),
         "miclip_row_norms": ([vp, i32, i32, vp, f32, vp, vp], ctypes.c_int),

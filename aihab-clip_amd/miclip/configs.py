@@ -27,11 +27,14 @@ class CLIPConfig:
     # "quick" = x*sigmoid(1.702x) (OpenAI CLIP, clip/model.py:160-162);
     # "erf" = exact GELU (open_clip ViT-H/14 shapes, stretch config C5).
     act: str = "quick"
+    # Vision head width: 64 in every OpenAI CLIP (clip/model.py:268 heads = width // 64);
+    # open_clip's ViT-H/14 runs 16 heads of 80 on width 1280.
+    vision_head_width: int = 64
 
     @property
     def vision_heads(self) -> int:
-        # clip/model.py:268
-        return self.vision_width // 64
+        # clip/model.py:268 (head_width 64); open_clip model configs name it directly
+        return self.vision_width // self.vision_head_width
 
     @property
     def grid(self) -> int:
@@ -63,6 +66,13 @@ MODEL_CONFIGS = {
                            vision_width=1024, vision_patch_size=14, **_TEXT_768),
     "ViT-L/14@336px": CLIPConfig(embed_dim=768, image_resolution=336, vision_layers=24,
                                  vision_width=1024, vision_patch_size=14, **_TEXT_768),
+    # open_clip "ViT-H-14" shapes (stretch config C5; the reference
+    # loads it through aihab_utils/model_init.py:42-112): same dual-encoder graph as
+    # OpenAI CLIP with exact-erf GELU in the MLPs and 80-wide vision heads.
+    "ViT-H-14": CLIPConfig(embed_dim=1024, image_resolution=224, vision_layers=32,
+                           vision_width=1280, vision_patch_size=14, context_length=77,
+                           vocab_size=49408, transformer_width=1024, transformer_heads=16,
+                           transformer_layers=24, act="erf", vision_head_width=80),
 }
 
 

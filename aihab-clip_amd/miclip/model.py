@@ -51,7 +51,8 @@ class _Handle:
             vocab_size=cfg.vocab_size, transformer_width=cfg.transformer_width,
             transformer_heads=cfg.transformer_heads, transformer_layers=cfg.transformer_layers,
             compute_dtype=compute_dtype,
-            act=_lib.MICLIP_ACT_GELU if cfg.act == "erf" else _lib.MICLIP_ACT_QUICKGELU)
+            act=_lib.MICLIP_ACT_GELU if cfg.act == "erf" else _lib.MICLIP_ACT_QUICKGELU,
+            vision_head_dim=cfg.vision_head_width)
         h = ctypes.c_void_p()
         _lib.check(self.lib.miclip_model_create(ctypes.byref(c), device_index, ctypes.byref(h)),
                    "miclip_model_create")

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MICLIP_ABI_VERSION 2
+#define MICLIP_ABI_VERSION 3
 
 enum miclip_status {
   MICLIP_OK = 0,
@@ -59,6 +59,8 @@ typedef struct miclip_config {
   int32_t transformer_layers;
   int32_t compute_dtype; /* miclip_dtype: GEMM/attention operand type (fp32 accumulate) */
   int32_t act;           /* miclip_act: QuickGELU (clip/model.py:160-162) or exact GELU */
+  int32_t vision_head_dim; /* 0 or 64: heads = width // 64 (clip/model.py:268); 80: open_clip
+                              ViT-H/14 (16 heads of 80 on width 1280) */
 } miclip_config;
 
 /* One host fp32 tensor of a CLIP state dict, named as in CLIP.state_dict(). */
@@ -176,7 +178,7 @@ int64_t miclip_model_bytes(const miclip_model* m);
 /* ---- diagnostics: per-kernel-class timing with HIP events ---- */
 
 /* Algorithmic totals of one kernel class since the last reset. `flops` counts
- * 2*M*N*K per GEMM and 4*N^2*64 per attention head; `bytes` is the minimum HBM
+ * 2*M*N*K per GEMM and 4*N^2*dh per attention head; `bytes` is the minimum HBM
  * traffic (operands read once, outputs written once). */
 typedef struct miclip_kernel_stat {
   const char* name;
@@ -209,13 +211,17 @@ int miclip_op_gemm(int32_t dtype, const void* A, const void* W, const float* bia
 int miclip_op_layernorm(int32_t dtype, const float* in, const float* gamma, const float* beta,
                         void* out, int32_t out_is_f32, int32_t R, int32_t D, void* stream);
 
-/* softmax(Q K^T / 8 + mask) V per head over a packed qkv [B*N, 3*H*64] buffer,
- * out [B*N, H*64]; replaces F.scaled_dot_product_attention inside
+/* softmax(Q K^T / sqrt(dh) + mask) V per head over a packed qkv [B*N, 3*H*dh]
+ * buffer, out [B*N, H*dh]; replaces F.scaled_dot_product_attention inside
  * nn.MultiheadAttention (clip/model.py:179-181), causal = text mask (323-329).
- * variant: 0 = default (pipelined multi-head kernel for N <= 320, else one
- * head per workgroup), 1 = one head per workgroup, 2 = pipelined. */
+ * head_dim dh: 64, or 80 (open_clip ViT-H/14 vision tower); 0 means 64.
+ * variant (dh 64): 0 = default (pipelined multi-head kernel for N <= 320, else
+ * one head per workgroup), 1 = one head per workgroup, 2 = pipelined,
+ * 4 = pipelined with the last-chunk split. dh 80 always runs one head per
+ * workgroup (N <= 416). */
 int miclip_op_attention(int32_t dtype, const void* qkv, void* out, int32_t B, int32_t N,
-                        int32_t H, int32_t causal, int32_t variant, void* stream);
+                        int32_t H, int32_t head_dim, int32_t causal, int32_t variant,
+                        void* stream);
 
 #ifdef __cplusplus
 }

@@ -22,6 +22,13 @@ the reference's LND layout, using the same torch ops in the same order, so it
 is bit-exact with the imported reference module on the same inputs
 (checked by `oracle/make_golden.py` and pinned by `tests/golden/*.npz`).
 
+ViT-H-14 (open_clip shapes): the same graph with exact GELU
+and 80-wide vision heads. open_clip itself is absent from the container and
+unpinned by the reference (configs/base.yaml names models, not a version), so
+this config is pinned against the reference's own clip/model.py modules with
+those two substitutions (`make_golden.py` vith14) -- "parity unpinned" with
+respect to open_clip's code.
+
 Parity pinning: the reference has no tests or golden vectors of its own
 (SURVEY §4). The goldens under tests/golden/ were produced by importing the
 reference `clip/model.py` in the build container and running it on the
@@ -45,6 +52,17 @@ def layer_norm(x, w, b):
 def quick_gelu(x):
     # clip/model.py:160-162
     return x * torch.sigmoid(1.702 * x)
+
+
+def gelu_erf(x):
+    # nn.GELU() (approximate='none'): the MLP activation of open_clip's
+    # ResidualAttentionBlock (act_layer default; open_clip is unpinned and absent
+    # here) -- ViT-H-14 config only
+    return F.gelu(x)
+
+
+def _act(name):
+    return gelu_erf if name == "erf" else quick_gelu
 
 
 def mha(x, in_w, in_b, out_w, out_b, heads, attn_mask=None):
@@ -73,15 +91,15 @@ def mha(x, in_w, in_b, out_w, out_b, heads, attn_mask=None):
     return o.view(L, B, o.size(1))
 
 
-def residual_block(x, sd, p, heads, attn_mask=None):
-    # clip/model.py:183-186
+def residual_block(x, sd, p, heads, attn_mask=None, act="quick"):
+    # clip/model.py:183-186 (act: clip/model.py:160-162 QuickGELU, or "erf")
     h = layer_norm(x, _t(sd, p + "ln_1.weight"), _t(sd, p + "ln_1.bias"))
     x = x + mha(h, _t(sd, p + "attn.in_proj_weight"), _t(sd, p + "attn.in_proj_bias"),
                 _t(sd, p + "attn.out_proj.weight"), _t(sd, p + "attn.out_proj.bias"),
                 heads, attn_mask)
     h = layer_norm(x, _t(sd, p + "ln_2.weight"), _t(sd, p + "ln_2.bias"))
     h = F.linear(h, _t(sd, p + "mlp.c_fc.weight"), _t(sd, p + "mlp.c_fc.bias"))
-    h = quick_gelu(h)
+    h = _act(act)(h)
     h = F.linear(h, _t(sd, p + "mlp.c_proj.weight"), _t(sd, p + "mlp.c_proj.bias"))
     return x + h
 
@@ -100,7 +118,8 @@ def encode_image(sd, cfg, images):
     x = layer_norm(x, _t(sd, "visual.ln_pre.weight"), _t(sd, "visual.ln_pre.bias"))
     x = x.permute(1, 0, 2)
     for i in range(cfg.vision_layers):
-        x = residual_block(x, sd, f"visual.transformer.resblocks.{i}.", cfg.vision_heads)
+        x = residual_block(x, sd, f"visual.transformer.resblocks.{i}.", cfg.vision_heads,
+                           act=cfg.act)
     x = x.permute(1, 0, 2)
     return layer_norm(x[:, 0, :], _t(sd, "visual.ln_post.weight"), _t(sd, "visual.ln_post.bias"))
 
@@ -123,7 +142,8 @@ def encode_text(sd, cfg, tokens):
     x = x.permute(1, 0, 2)
     mask = causal_mask(cfg.context_length)
     for i in range(cfg.transformer_layers):
-        x = residual_block(x, sd, f"transformer.resblocks.{i}.", cfg.transformer_heads, mask)
+        x = residual_block(x, sd, f"transformer.resblocks.{i}.", cfg.transformer_heads, mask,
+                           act=cfg.act)
     x = x.permute(1, 0, 2)
     x = layer_norm(x, _t(sd, "ln_final.weight"), _t(sd, "ln_final.bias"))
     x_before = x[torch.arange(x.shape[0]), text.argmax(dim=-1)]

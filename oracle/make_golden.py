@@ -80,17 +80,36 @@ def tokenize(tokenizer, texts, context_length=77):
     return out
 
 
-def reference_model(refmodel, sd_np):
+def reference_model(refmodel, sd_np, cfg=None):
     sd = {k: torch.from_numpy(v.copy()) for k, v in sd_np.items()}
-    m = refmodel.build_model(sd)          # fp16 convert + load_state_dict + eval
-    return m.float()                       # clip/clip.py:135-136 (CPU path)
+    if cfg is None or (cfg.act == "quick" and cfg.vision_head_width == 64):
+        m = refmodel.build_model(sd)      # fp16 convert + load_state_dict + eval
+        return m.float()                   # clip/clip.py:135-136 (CPU path)
+    # open_clip ViT-H-14 shapes: build_model's graph
+    # (clip/model.py:421-433) with the two open_clip differences substituted --
+    # the vision tower built with 80-wide heads (CLIP.__init__ hard-codes
+    # width // 64 at clip/model.py:267) and nn.GELU in every MLP (QuickGELU at
+    # clip/model.py:173). open_clip itself is absent, so this pins our oracle to
+    # the reference's modules, not to open_clip's code.
+    m = refmodel.CLIP(cfg.embed_dim, cfg.image_resolution, cfg.vision_layers, cfg.vision_width,
+                      cfg.vision_patch_size, cfg.context_length, cfg.vocab_size,
+                      cfg.transformer_width, cfg.transformer_heads, cfg.transformer_layers)
+    m.visual = refmodel.VisionTransformer(cfg.image_resolution, cfg.vision_patch_size,
+                                          cfg.vision_width, cfg.vision_layers, cfg.vision_heads,
+                                          cfg.embed_dim)
+    if cfg.act == "erf":
+        for blk in list(m.visual.transformer.resblocks) + list(m.transformer.resblocks):
+            blk.mlp.gelu = torch.nn.GELU()
+    refmodel.convert_weights(m)
+    m.load_state_dict(sd)
+    return m.eval().float()
 
 
 def run_config(tag, model_name, n_images, prompts, refs, seed=0):
     refmodel, tok_mod, _, _ = refs
     cfg = MODEL_CONFIGS[model_name]
     sd = generate_state_dict(cfg, seed=seed)
-    model = reference_model(refmodel, sd)
+    model = reference_model(refmodel, sd, cfg)
     tokenizer = tok_mod.SimpleTokenizer()
     tokens = tokenize(tokenizer, prompts)
     imgs = synthetic_images(n_images, cfg.image_resolution, seed=seed)
@@ -149,7 +168,7 @@ def run_config(tag, model_name, n_images, prompts, refs, seed=0):
     return diffs
 
 
-def main():
+def main(only=None):
     refs = reference_modules()
     _, _, data, templates = refs
     os.makedirs(OUT, exist_ok=True)
@@ -160,13 +179,16 @@ def main():
         hier, _ = templates.gen_prompts(True, True)                    # data/templates.py:236
     c1_prompts = flat[:10]
     all_diffs = {}
-    all_diffs["vitb32"] = run_config("vitb32", "ViT-B/32", 8, c1_prompts, refs)
-    all_diffs["vitb16"] = run_config("vitb16", "ViT-B/16", 4, flat, refs)
-    all_diffs["vitl14"] = run_config("vitl14", "ViT-L/14", 4, hier, refs)
-    all_diffs["vitl14_336"] = run_config("vitl14_336", "ViT-L/14@336px", 2, hier, refs)
+    jobs = [("vitb32", "ViT-B/32", 8, c1_prompts), ("vitb16", "ViT-B/16", 4, flat),
+            ("vitl14", "ViT-L/14", 4, hier), ("vitl14_336", "ViT-L/14@336px", 2, hier),
+            ("vith14", "ViT-H-14", 2, c1_prompts)]
+    for tag, name, n, prompts in jobs:
+        if only and tag not in only:
+            continue
+        all_diffs[tag] = run_config(tag, name, n, prompts, refs)
     worst = max(max(d.values()) for d in all_diffs.values())
     print(f"[golden] worst oracle-vs-reference max|d| over all outputs: {worst:.3e}")
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:] or None)   # optional tags, e.g. `make_golden.py vith14`

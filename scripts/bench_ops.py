@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--width", type=int, default=1024)
     ap.add_argument("--tokens", type=int, default=257)
+    ap.add_argument("--head-dim", type=int, default=64, help="attention head dim (64, or 80 = ViT-H/14)")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--variants", default="128,256")
     ap.add_argument("--ops", default="gemm,attention,layernorm")
@@ -93,17 +94,18 @@ def main():
                 del a_, w_
         del A, Wt, C16, X
     if "attention" in args.ops:
-        H = W // 64
+        dh = args.head_dim
+        H = W // dh
         qkv = (torch.randn(M, 3 * W, device="cuda", generator=g)).to(dt)
         o = torch.empty(M, W, device="cuda", dtype=dt)
 
-        for av in (1, 2, 4, 1, 2, 4):
+        for av in ((1, 2, 4, 1, 2, 4) if dh == 64 else (0, 0)):
             def fa():
-                rc = lib.miclip_op_attention(0, qkv.data_ptr(), o.data_ptr(), args.batch, args.tokens, H, 0,
-                                             av, s)
+                rc = lib.miclip_op_attention(0, qkv.data_ptr(), o.data_ptr(), args.batch, args.tokens, H, dh,
+                                             0, av, s)
                 assert rc == 0
             ms = timeit(fa, args.iters)
-            fl = 4.0 * args.batch * H * args.tokens ** 2 * 64
+            fl = 4.0 * args.batch * H * args.tokens ** 2 * dh
             out.append(dict(op="attention", variant=av, B=args.batch, N=args.tokens, H=H, ms=round(ms, 4),
                             tflops=round(fl / ms / 1e9, 1), gbs=round(4.0 * M * W * 2 / ms / 1e6, 1)))
             print(json.dumps(out[-1]), flush=True)

@@ -52,7 +52,7 @@ def test_nm_shows_c_linkage():
 
 def test_abi_version_and_validation(lib):
     from miclip import _lib
-    assert lib.miclip_abi_version() == 2
+    assert lib.miclip_abi_version() == _lib.ABI_VERSION == 3
     bad = _lib.MiclipConfig(embed_dim=512, image_resolution=224, vision_layers=12, vision_width=700,
                             vision_patch_size=32, context_length=77, vocab_size=49408,
                             transformer_width=512, transformer_heads=8, transformer_layers=12,
@@ -61,6 +61,13 @@ def test_abi_version_and_validation(lib):
     rc = lib.miclip_model_create(ctypes.byref(bad), 0, ctypes.byref(h))
     assert rc == -1
     assert b"vision_width" in lib.miclip_last_error()
+    # open_clip ViT-H/14 heads (80) are accepted, other head widths are not
+    bad_dh = _lib.MiclipConfig(embed_dim=1024, image_resolution=224, vision_layers=32,
+                               vision_width=1280, vision_patch_size=14, context_length=77,
+                               vocab_size=49408, transformer_width=1024, transformer_heads=16,
+                               transformer_layers=24, compute_dtype=0, act=2, vision_head_dim=96)
+    assert lib.miclip_model_create(ctypes.byref(bad_dh), 0, ctypes.byref(h)) == -1
+    assert b"vision_head_dim" in lib.miclip_last_error()
     assert lib.miclip_model_create(None, 0, ctypes.byref(h)) == -1
     assert lib.miclip_op_gemm(0, None, None, None, None, 1, 128, 64, 0, 0, 0, None) == -1
     lib.miclip_model_destroy(None)           # no-op on NULL

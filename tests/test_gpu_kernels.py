@@ -146,13 +146,13 @@ def test_layernorm(lib, dt, R, D):
     assert (outt.float() - ref).abs().max().item() < (3e-2 if dt == "bf16" else 4e-3)
 
 
-def _attn_ref(qkv, B, N, H, causal):
-    q, k, v = qkv.float().view(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+def _attn_ref(qkv, B, N, H, causal, dh=64):
+    q, k, v = qkv.float().view(B, N, 3, H, dh).permute(2, 0, 3, 1, 4)
     mask = None
     if causal:
         mask = torch.full((N, N), float("-inf"), device=qkv.device).triu_(1)
     o = torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=mask)
-    return o.permute(0, 2, 1, 3).reshape(B * N, H * 64)
+    return o.permute(0, 2, 1, 3).reshape(B * N, H * dh)
 
 
 @pytest.mark.parametrize("variant", [1, 2, 4])
@@ -166,8 +166,8 @@ def test_attention(lib, dt, B, N, H, causal, variant):
     g = torch.Generator(device="cuda").manual_seed(B * 1000 + N + H + causal)
     qkv = (torch.randn(B * N, 3 * H * 64, device="cuda", generator=g) * 1.5).to(tdt)
     out = torch.empty(B * N, H * 64, device="cuda", dtype=tdt)
-    _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), out.data_ptr(), B, N, H, causal, variant,
-                                        _stream()))
+    _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), out.data_ptr(), B, N, H, 64, causal,
+                                        variant, _stream()))
     torch.cuda.synchronize()
     ref = _attn_ref(qkv, B, N, H, causal)
     err = (out.float() - ref).abs().max().item()
@@ -182,7 +182,34 @@ def test_attention_spike(lib):
     qkv[200, 64:128] = 2.0       # key 200 in the 7th key tile -> max jumps late
     qkv = qkv.half()
     out = torch.empty(B * N, 64, device="cuda", dtype=torch.float16)
-    _check(lib, lib.miclip_op_attention(0, qkv.data_ptr(), out.data_ptr(), B, N, H, 0, 0, _stream()))
+    _check(lib, lib.miclip_op_attention(0, qkv.data_ptr(), out.data_ptr(), B, N, H, 0, 0, 0,
+                                        _stream()))
     torch.cuda.synchronize()
     ref = _attn_ref(qkv, B, N, H, 0)
     assert (out.float() - ref).abs().max().item() < 6e-3
+
+
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+@pytest.mark.parametrize("B,N,H,causal", [(2, 257, 16, 0), (1, 50, 3, 0), (3, 77, 2, 1),
+                                          (1, 1, 1, 0), (2, 100, 2, 1), (1, 416, 2, 0),
+                                          (5, 197, 4, 0)])
+def test_attention_dh80(lib, dt, B, N, H, causal):
+    """Head dim 80 (open_clip ViT-H/14: 16 heads on width 1280); scale 1/sqrt(80)."""
+    code, tdt = DT[dt]
+    g = torch.Generator(device="cuda").manual_seed(B * 1000 + N + H + causal + 80)
+    qkv = (torch.randn(B * N, 3 * H * 80, device="cuda", generator=g) * 1.5).to(tdt)
+    # canary past the output: the padding dims 80..95 must never be stored
+    out = torch.full((B * N + 1, H * 80), 7.0, device="cuda", dtype=tdt)
+    _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), out.data_ptr(), B, N, H, 80, causal,
+                                        0, _stream()))
+    torch.cuda.synchronize()
+    ref = _attn_ref(qkv, B, N, H, causal, dh=80)
+    err = (out[:B * N].float() - ref).abs().max().item()
+    assert err < (4e-2 if dt == "bf16" else 6e-3), err
+    assert bool((out[B * N] == 7.0).all())
+
+
+def test_attention_bad_head_dim(lib):
+    x = torch.zeros(3 * 96, device="cuda", dtype=torch.float16)
+    y = torch.zeros(96, device="cuda", dtype=torch.float16)
+    assert lib.miclip_op_attention(0, x.data_ptr(), y.data_ptr(), 1, 1, 1, 96, 0, 0, _stream()) != 0

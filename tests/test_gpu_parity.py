@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 COS_TOL = 1e-3
 CONFIGS = [("vitb32", "ViT-B/32"), ("vitb16", "ViT-B/16"), ("vitl14", "ViT-L/14"),
-           ("vitl14_336", "ViT-L/14@336px")]
+           ("vitl14_336", "ViT-L/14@336px"), ("vith14", "ViT-H-14")]
 
 
 def _one_minus_cos(a, b):
@@ -69,7 +69,7 @@ def test_encode_image_matches_reference(golden, tag, name, dtype):
 
 
 @pytest.mark.parametrize("dtype", ["fp16", "bf16"])
-@pytest.mark.parametrize("tag,name", CONFIGS[:3])
+@pytest.mark.parametrize("tag,name", CONFIGS[:3] + CONFIGS[4:])
 def test_encode_text_matches_reference(golden, tag, name, dtype):
     g = golden(tag)
     m = _model(name, dtype)

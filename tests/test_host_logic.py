@@ -14,7 +14,9 @@ from miclip.weights import param_specs
 REF_BPE = "/root/reference/clip/bpe_simple_vocab_16e6.txt.gz"
 
 
-@pytest.mark.parametrize("name", list(MODEL_CONFIGS))
+# build_model's shape inference (clip/model.py:396-419) only covers OpenAI CLIP
+# checkpoints; the open_clip ViT-H-14 entry (GELU, 80-wide heads) is name-only.
+@pytest.mark.parametrize("name", [n for n, c in MODEL_CONFIGS.items() if c.act == "quick"])
 def test_config_inference_roundtrip(name):
     cfg = MODEL_CONFIGS[name]
     fake = {n: np.empty(shape, dtype=np.float32) for n, shape, _, _ in param_specs(cfg)}

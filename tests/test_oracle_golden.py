@@ -14,7 +14,7 @@ from miclip.weights import generate_state_dict, synthetic_images, checksum
 from oracle import clip_oracle
 
 TAGS = {"vitb32": "ViT-B/32", "vitb16": "ViT-B/16", "vitl14": "ViT-L/14",
-        "vitl14_336": "ViT-L/14@336px"}
+        "vitl14_336": "ViT-L/14@336px", "vith14": "ViT-H-14"}
 
 
 @pytest.fixture(scope="module")
@@ -40,7 +40,7 @@ def test_generator_matches_fixture(golden, states, tag):
     assert checksum(imgs) == g["meta"]["image_crc"]
 
 
-@pytest.mark.parametrize("tag", ["vitb32", "vitb16", "vitl14"])
+@pytest.mark.parametrize("tag", ["vitb32", "vitb16", "vitl14", "vith14"])
 def test_oracle_image_bit_exact(golden, states, tag):
     torch.set_num_threads(8)
     g = golden(tag)
@@ -51,7 +51,7 @@ def test_oracle_image_bit_exact(golden, states, tag):
     assert np.abs(out - g["image"]).max() <= 1e-6
 
 
-@pytest.mark.parametrize("tag", ["vitb32", "vitl14"])
+@pytest.mark.parametrize("tag", ["vitb32", "vitl14", "vith14"])
 def test_oracle_text_and_head(golden, states, tag):
     g = golden(tag)
     cfg = MODEL_CONFIGS[TAGS[tag]]
