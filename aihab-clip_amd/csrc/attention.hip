@@ -229,9 +229,10 @@ MICLIP_DEV void load_q(i16x8 (&qf)[HeadGeom<DH>::NKS], const T* base, int ld, in
 
 // One workgroup per (image, head). Launch bounds: 10 waves for DH = 64 (3
 // per SIMD, ~165 VGPRs); DH = 80 carries a third O^T tile and a fifth Q
-// fragment, so 8 waves (2 per SIMD, up to 256 VGPRs).
+// fragment and just fits the 168 VGPRs of 9 waves (3 on one SIMD): one wave
+// per 32-query chunk at N = 257 (8 waves left one wave two chunks).
 template <typename T, bool CAUSAL, int DH>
-__global__ __launch_bounds__(DH == 64 ? 640 : 512) void attention_kernel(
+__global__ __launch_bounds__(DH == 64 ? 640 : 576) void attention_kernel(
     const T* __restrict__ qkv, T* __restrict__ out, int N, int H, int Npad, int nchunks,
     float qk_scale) {
   using G = HeadGeom<DH>;
@@ -444,8 +445,8 @@ hipError_t attn_launch_plain(const void* qkv, void* out, int B, int N, int H, hi
   const int nchunks = Npad / 32;
   const size_t lds = (size_t)Npad * G::ROWB * 2;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  // at most 10 (DH 64) / 8 (DH 80) waves, see attention_kernel's launch bounds
-  constexpr int maxw = DH == 64 ? 10 : 8;
+  // at most 10 (DH 64) / 9 (DH 80) waves, see attention_kernel's launch bounds
+  constexpr int maxw = DH == 64 ? 10 : 9;
   const int per = (nchunks + maxw - 1) / maxw;
   const int nw = (nchunks + per - 1) / per;
   auto kern = attention_kernel<T, CAUSAL, DH>;

@@ -79,7 +79,7 @@ NO_TAIL = 1 << 16   # gemm.hip kGemmNoTail: every row in 256x256 tiles
                                    (16448, 3072, 256), (16500, 1024, 2048), (4352, 4096, 512),
                                    (4296, 4096, 256), (16640, 3072, 256)])
 @pytest.mark.parametrize("variant", [258, 260, 256, 258 | (1 << 17), 260 | (1 << 17)])
-@pytest.mark.parametrize("epi,act", [(0, 0), (0, 1), (1, 0), (2, 0)])
+@pytest.mark.parametrize("epi,act", [(0, 0), (0, 1), (0, 2), (1, 0), (2, 0)])
 def test_gemm_tail_bitexact(lib, dt, M, N, K, variant, epi, act):
     """Row tail of a 256x256 launch (rows past the last whole round of tiles,
     computed as 16-row slivers of tiles (SCHED 2) or by tail workgroups) equals the all-tile launch bit for bit
@@ -107,6 +107,8 @@ def test_gemm_tail_bitexact(lib, dt, M, N, K, variant, epi, act):
     ref = A[-300:].float() @ W.float().t() + bias
     if epi == 0 and act == 1:
         ref = ref * torch.sigmoid(1.702 * ref)
+    if epi == 0 and act == 2:
+        ref = torch.nn.functional.gelu(ref)
     if epi == 1:
         ref = X0[-300:] + ref
     err = (outs[0][-300:].float() - ref).abs().max().item()
