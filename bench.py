@@ -200,7 +200,8 @@ def main():
                         traffic = t.get("hbm_bytes_per_launch")
                 except (OSError, ValueError):
                     traffic = None
-            roofline = {"bound": "mfma", "kernel": "gemm_fc (MLP c_fc + QuickGELU epilogue)",
+            act_name = "exact-GELU" if cfg.act == "erf" else "QuickGELU"
+            roofline = {"bound": "mfma", "kernel": f"gemm_fc (MLP c_fc + {act_name} epilogue)",
                         "achieved": round(achieved, 1), "peak": round(PEAK_TFLOPS, 1),
                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_TFLOPS, 4),
                         "traffic": traffic,
