@@ -17,6 +17,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -81,7 +82,7 @@ struct Workspace {
   int cap_rows = 0;   // token rows
   int cap_items = 0;  // images or prompts
   void* patches = nullptr;
-  float* x = nullptr;
+  void* x = nullptr;  // residual stream: fp32, or fp16 (miclip_model::resid16)
   void* h = nullptr;
   void* qkv = nullptr;
   void* o = nullptr;
@@ -96,6 +97,11 @@ struct miclip_model {
   miclip_config cfg{};
   int device = 0;
   int dtype = 0;
+  // fp16 residual stream (x between blocks), the reference's own fp16 GPU model
+  // (clip.load on cuda: convert_weights, clip/model.py:372-393, and the half
+  // activations of VisionTransformer / Transformer). Default with fp16 compute;
+  // MICLIP_RESID_F32=1 keeps an fp32 stream. bf16 compute always streams fp32.
+  int resid16 = 0;
   int Kp = 0;  // padded patch-GEMM K
   std::unordered_map<void*, size_t> allocs;
   int64_t bytes = 0;
@@ -246,7 +252,7 @@ int ensure_ws(miclip_model* m, Workspace& w, int items, int ntok, int W, bool im
     const int g = m->cfg.image_resolution / m->cfg.vision_patch_size;
     if ((rc = dev_alloc(m, &w.patches, (size_t)items * g * g * m->Kp * e))) return rc;
   }
-  if ((rc = dev_alloc(m, (void**)&w.x, (size_t)rows * W * 4))) return rc;
+  if ((rc = dev_alloc(m, &w.x, (size_t)rows * W * (m->resid16 ? 2 : 4)))) return rc;
   if ((rc = dev_alloc(m, &w.h, (size_t)rows * W * e))) return rc;
   if ((rc = dev_alloc(m, &w.qkv, (size_t)rows * 3 * W * e))) return rc;
   if ((rc = dev_alloc(m, &w.o, (size_t)rows * W * e))) return rc;
@@ -267,11 +273,12 @@ double gemm_bytes(double M, double N, double K, double c_bytes) {
 
 int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, int W, int H,
               int dh, int causal, hipStream_t s) {
-  const int M = items * N, dt = m->dtype;
-  const double dM = M, dW = W;
+  const int M = items * N, dt = m->dtype, r16 = m->resid16;
+  const double dM = M, dW = W, rb = r16 ? 2 : 4;  // residual bytes per element
   {
-    ProfScope p(m, K_LAYERNORM, s, 0, dM * dW * 6);
-    MICLIP_HIP(layernorm(dt, w.x, nullptr, 1, b.ln1_g, b.ln1_b, nullptr, w.h, M, W, 0, s));
+    ProfScope p(m, K_LAYERNORM, s, 0, dM * dW * (rb + 2));
+    MICLIP_HIP(
+        layernorm(dt, w.x, nullptr, 1, b.ln1_g, b.ln1_b, nullptr, w.h, M, W, 0, s, r16));
   }
   {
     ProfScope p(m, K_GEMM_QKV, s, gemm_flops(dM, 3 * dW, dW), gemm_bytes(dM, 3 * dW, dW, 2));
@@ -283,20 +290,22 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
     MICLIP_HIP(attention(dt, w.qkv, w.o, items, N, H, causal, s, 0, dh));
   }
   {
-    ProfScope p(m, K_GEMM_OUT, s, gemm_flops(dM, dW, dW), gemm_bytes(dM, dW, dW, 8));
-    MICLIP_HIP(gemm_residual(dt, w.o, b.w_out, b.b_out, w.x, M, W, W, s));
+    ProfScope p(m, K_GEMM_OUT, s, gemm_flops(dM, dW, dW), gemm_bytes(dM, dW, dW, 2 * rb));
+    MICLIP_HIP(gemm_residual(dt, w.o, b.w_out, b.b_out, w.x, M, W, W, s, 0, r16));
   }
   {
-    ProfScope p(m, K_LAYERNORM, s, 0, dM * dW * 6);
-    MICLIP_HIP(layernorm(dt, w.x, nullptr, 1, b.ln2_g, b.ln2_b, nullptr, w.h, M, W, 0, s));
+    ProfScope p(m, K_LAYERNORM, s, 0, dM * dW * (rb + 2));
+    MICLIP_HIP(
+        layernorm(dt, w.x, nullptr, 1, b.ln2_g, b.ln2_b, nullptr, w.h, M, W, 0, s, r16));
   }
   {
     ProfScope p(m, K_GEMM_FC, s, gemm_flops(dM, 4 * dW, dW), gemm_bytes(dM, 4 * dW, dW, 2));
     MICLIP_HIP(gemm_store(dt, w.h, b.w_fc, b.b_fc, w.f, M, 4 * W, W, m->cfg.act, s));
   }
   {
-    ProfScope p(m, K_GEMM_PROJ, s, gemm_flops(dM, dW, 4 * dW), gemm_bytes(dM, dW, 4 * dW, 8));
-    MICLIP_HIP(gemm_residual(dt, w.f, b.w_proj, b.b_proj, w.x, M, W, 4 * W, s));
+    ProfScope p(m, K_GEMM_PROJ, s, gemm_flops(dM, dW, 4 * dW),
+                gemm_bytes(dM, dW, 4 * dW, 2 * rb));
+    MICLIP_HIP(gemm_residual(dt, w.f, b.w_proj, b.b_proj, w.x, M, W, 4 * W, s, 0, r16));
   }
   return 0;
 }
@@ -308,7 +317,7 @@ Workspace view(const miclip_model* m, const Workspace& w, size_t row0, size_t it
   const size_t e = elt();
   const int g = m->cfg.image_resolution / m->cfg.vision_patch_size;
   if (w.patches) v.patches = (char*)w.patches + item0 * g * g * m->Kp * e;
-  v.x = w.x + row0 * W;
+  v.x = (char*)w.x + row0 * W * (m->resid16 ? 2 : 4);
   v.h = (char*)w.h + row0 * W * e;
   v.qkv = (char*)w.qkv + row0 * 3 * W * e;
   v.o = (char*)w.o + row0 * W * e;
@@ -343,13 +352,19 @@ int encode_image_part(miclip_model* m, Workspace w, const float* images, int B, 
   }
   {
     const double dM = (double)B * np;
-    ProfScope p(m, K_GEMM_PATCH, s, gemm_flops(dM, W, 3.0 * P * P), gemm_bytes(dM, W, m->Kp, 4));
-    MICLIP_HIP(gemm_patch(dt, w.patches, m->conv_w, m->vpos, w.x, B * np, W, m->Kp, np, s));
+    const int rb = m->resid16 ? 2 : 4;
+    ProfScope p(m, K_GEMM_PATCH, s, gemm_flops(dM, W, 3.0 * P * P),
+                gemm_bytes(dM, W, m->Kp, rb));
+    MICLIP_HIP(gemm_patch(dt, w.patches, m->conv_w, m->vpos, w.x, B * np, W, m->Kp, np, s,
+                          m->resid16));
   }
   {
-    ProfScope p(m, K_LAYERNORM, s, 0, (double)M * W * 8);
-    MICLIP_HIP(class_token(m->cls, m->vpos, w.x, B, N, W, s));
-    MICLIP_HIP(layernorm(dt, w.x, nullptr, 1, m->ln_pre_g, m->ln_pre_b, w.x, nullptr, M, W, 0, s));
+    ProfScope p(m, K_LAYERNORM, s, 0, (double)M * W * (m->resid16 ? 4 : 8));
+    MICLIP_HIP(class_token(m->cls, m->vpos, w.x, B, N, W, s, m->resid16));
+    // ln_pre in place: fp32 stream -> fp32 out; fp16 stream -> compute-dtype (fp16) out
+    MICLIP_HIP(layernorm(dt, w.x, nullptr, 1, m->ln_pre_g, m->ln_pre_b,
+                         m->resid16 ? nullptr : (float*)w.x, m->resid16 ? w.x : nullptr, M, W,
+                         0, s, m->resid16));
   }
   for (int l = 0; l < c.vision_layers; ++l)
     if ((rc = run_block(m, m->vblocks[l], w, B, N, W, H, dh, 0, s))) return rc;
@@ -358,10 +373,10 @@ int encode_image_part(miclip_model* m, Workspace w, const float* images, int B, 
   ProfScope p(m, K_HEAD, s, proj ? 2.0 * B * W * c.embed_dim : 0.0, (double)B * W * 8);
   if (!proj) {
     MICLIP_HIP(layernorm(dt, w.x, nullptr, N, m->ln_post_g, m->ln_post_b, out, nullptr, B, W,
-                         norm ? 1 : 0, s));
+                         norm ? 1 : 0, s, m->resid16));
   } else {
     MICLIP_HIP(layernorm(dt, w.x, nullptr, N, m->ln_post_g, m->ln_post_b, w.feat, nullptr, B, W,
-                         0, s));
+                         0, s, m->resid16));
     MICLIP_HIP(rowvec_matmul(w.feat, m->vproj, out, B, W, c.embed_dim, s));
     if (norm) MICLIP_HIP(row_l2norm(out, B, c.embed_dim, s));
   }
@@ -416,6 +431,10 @@ int miclip_model_create(const miclip_config* cfg, int device, miclip_model** out
   m->cfg = c;
   m->device = device;
   m->dtype = cfg->compute_dtype;
+  {
+    const char* e = getenv("MICLIP_RESID_F32");
+    m->resid16 = m->dtype == MICLIP_FP16 && !(e && atoi(e) != 0);
+  }
   const int P = cfg->vision_patch_size, Wv = cfg->vision_width, Wt = cfg->transformer_width;
   m->Kp = (3 * P * P + 63) / 64 * 64;
   const int g = cfg->image_resolution / P, N = g * g + 1, E = cfg->embed_dim;
@@ -568,14 +587,15 @@ int miclip_encode_text(miclip_model* m, const int64_t* tokens, int32_t P, float*
   Workspace& w = m->wtxt;
   {
     ProfScope p(m, K_TEXT_EMBED, s, 0, (double)P * L * W * 12);
-    MICLIP_HIP(token_embed(tokens, m->tok_emb, m->tpos, w.x, w.rows, P, L, W, c.vocab_size, s));
+    MICLIP_HIP(token_embed(tokens, m->tok_emb, m->tpos, w.x, w.rows, P, L, W, c.vocab_size, s,
+                           m->resid16));
   }
   for (int l = 0; l < c.transformer_layers; ++l)
     if ((rc = run_block(m, m->tblocks[l], w, P, L, W, H, 64, 1, s))) return rc;
   float* xb = x_before ? x_before : w.feat;
   ProfScope p(m, K_HEAD, s, x_proj ? 2.0 * P * W * c.embed_dim : 0.0, (double)P * W * 8);
   MICLIP_HIP(layernorm(m->dtype, w.x, w.rows, 0, m->ln_final_g, m->ln_final_b, xb, nullptr, P, W,
-                       0, s));
+                       0, s, m->resid16));
   if (x_proj) MICLIP_HIP(rowvec_matmul(xb, m->text_proj, x_proj, P, W, c.embed_dim, s));
   return 0;
 }
@@ -714,17 +734,21 @@ int miclip_op_gemm(int32_t dtype, const void* A, const void* W, const float* bia
     MICLIP_HIP(gemm_f32(dtype, A, W, bias, (float*)C, M, N, K, s, variant));
   } else if (epi == 3) {
     MICLIP_HIP(gemm_null(dtype, A, W, (float*)C, M, N, K, s, variant));
+  } else if (epi == 4) {
+    if (!bias) return fail(MICLIP_EINVAL, "residual epilogue needs a bias");
+    MICLIP_HIP(gemm_residual(dtype, A, W, bias, C, M, N, K, s, variant, 1));
   } else {
     return fail(MICLIP_EINVAL, "unknown epilogue");
   }
   return 0;
 }
 
-int miclip_op_layernorm(int32_t dtype, const float* in, const float* gamma, const float* beta,
-                        void* out, int32_t out_is_f32, int32_t R, int32_t D, void* stream) {
+int miclip_op_layernorm(int32_t dtype, const void* in, const float* gamma, const float* beta,
+                        void* out, int32_t flags, int32_t R, int32_t D, void* stream) {
   if (!in || !gamma || !beta || !out) return fail(MICLIP_EINVAL, "null argument");
-  MICLIP_HIP(layernorm(dtype, in, nullptr, 1, gamma, beta, out_is_f32 ? (float*)out : nullptr,
-                       out_is_f32 ? nullptr : out, R, D, 0, (hipStream_t)stream));
+  const bool of32 = flags & 1;
+  MICLIP_HIP(layernorm(dtype, in, nullptr, 1, gamma, beta, of32 ? (float*)out : nullptr,
+                       of32 ? nullptr : out, R, D, 0, (hipStream_t)stream, (flags >> 1) & 1));
   return 0;
 }
 

@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #define MICLIP_DEV __device__ __forceinline__
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));

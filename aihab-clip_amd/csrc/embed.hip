@@ -38,26 +38,28 @@ __global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ i
   }
 }
 
+// R: residual-stream type (float, or _Float16 for the fp16 stream)
+template <typename R>
 __global__ __launch_bounds__(256) void class_token_kernel(const float* __restrict__ cls,
                                                           const float* __restrict__ pos,
-                                                          float* __restrict__ X, int ntok,
-                                                          int D) {
-  float* dst = X + (size_t)blockIdx.x * ntok * D;
-  for (int d = threadIdx.x; d < D; d += blockDim.x) dst[d] = cls[d] + pos[d];
+                                                          R* __restrict__ X, int ntok, int D) {
+  R* dst = X + (size_t)blockIdx.x * ntok * D;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) dst[d] = (R)(cls[d] + pos[d]);
 }
 
+template <typename R>
 __global__ __launch_bounds__(256) void token_embed_kernel(const int64_t* __restrict__ tokens,
                                                           const float* __restrict__ emb,
                                                           const float* __restrict__ pos,
-                                                          float* __restrict__ X, int L, int D,
+                                                          R* __restrict__ X, int L, int D,
                                                           int vocab) {
   const int row = blockIdx.x, t = row % L;
   int64_t id = tokens[row];
   id = id < 0 ? 0 : (id >= vocab ? vocab - 1 : id);  // ids are validated on the host
   const float* e = emb + (size_t)id * D;
   const float* p = pos + (size_t)t * D;
-  float* dst = X + (size_t)row * D;
-  for (int d = threadIdx.x; d < D; d += blockDim.x) dst[d] = e[d] + p[d];
+  R* dst = X + (size_t)row * D;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) dst[d] = (R)(e[d] + p[d]);
 }
 
 // one wave per prompt: first index of the maximum token id (torch.argmax)
@@ -264,17 +266,27 @@ hipError_t im2col(int dtype, const float* img, void* patches, int B, int R, int 
   return hipGetLastError();
 }
 
-hipError_t class_token(const float* cls, const float* pos, float* X, int B, int ntok, int D,
-                       hipStream_t s) {
-  hipLaunchKernelGGL(class_token_kernel, dim3(B), dim3(256), 0, s, cls, pos, X, ntok, D);
+hipError_t class_token(const float* cls, const float* pos, void* X, int B, int ntok, int D,
+                       hipStream_t s, int resid16) {
+  if (resid16)
+    hipLaunchKernelGGL(class_token_kernel<_Float16>, dim3(B), dim3(256), 0, s, cls, pos,
+                       (_Float16*)X, ntok, D);
+  else
+    hipLaunchKernelGGL(class_token_kernel<float>, dim3(B), dim3(256), 0, s, cls, pos, (float*)X,
+                       ntok, D);
   return hipGetLastError();
 }
 
-hipError_t token_embed(const int64_t* tokens, const float* tok_emb, const float* pos, float* X,
-                       int32_t* eot_rows, int P, int L, int D, int vocab, hipStream_t s) {
+hipError_t token_embed(const int64_t* tokens, const float* tok_emb, const float* pos, void* X,
+                       int32_t* eot_rows, int P, int L, int D, int vocab, hipStream_t s,
+                       int resid16) {
   if (P < 1 || L < 1) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(token_embed_kernel, dim3(P * L), dim3(256), 0, s, tokens, tok_emb, pos, X,
-                     L, D, vocab);
+  if (resid16)
+    hipLaunchKernelGGL(token_embed_kernel<_Float16>, dim3(P * L), dim3(256), 0, s, tokens,
+                       tok_emb, pos, (_Float16*)X, L, D, vocab);
+  else
+    hipLaunchKernelGGL(token_embed_kernel<float>, dim3(P * L), dim3(256), 0, s, tokens, tok_emb,
+                       pos, (float*)X, L, D, vocab);
   hipLaunchKernelGGL(eot_kernel, dim3(P), dim3(64), 0, s, tokens, eot_rows, L);
   return hipGetLastError();
 }

@@ -166,27 +166,53 @@ struct EpiStore {
   }
 };
 
+// Residual stream X (R = float, or _Float16 as in the reference's fp16 GPU
+// model, clip/model.py:184-185 `x = x + ...` on half tensors) += acc + bias.
+// fp16: one rounding of x + (acc + bias) (the reference rounds acc + bias
+// first), pinned by fin so the tile and tail paths round alike.
+template <typename R>
 struct EpiResidual {
-  float* X;
+  R* X;
   const float* bias;
   int ldx;
   MICLIP_DEV float4 bias4(int col) const { return ld_bias4(bias, col); }
   MICLIP_DEV float4 bias4nb(int col) const { return ld_bias4_nb(bias, col); }
   MICLIP_DEV float bias1(int col) const { return bias[col]; }
+  MICLIP_DEV static float fin(float y) {
+    asm volatile("" : "+v"(y));
+    return y;
+  }
   template <bool ASM = false>
   MICLIP_DEV void put4(int r, int c, float4 v, float4 b) const {
-    float4* p = (float4*)(X + (size_t)r * ldx + c);
-    const float4 x = *p;
-    const float4 y =
-        make_float4(x.x + (v.x + b.x), x.y + (v.y + b.y), x.z + (v.z + b.z), x.w + (v.w + b.w));
-    if constexpr (ASM)
-      st_b128_asm(p, y);
-    else
-      *p = y;
+    if constexpr (std::is_same_v<R, float>) {
+      float4* p = (float4*)(X + (size_t)r * ldx + c);
+      const float4 x = *p;
+      const float4 y = make_float4(x.x + (v.x + b.x), x.y + (v.y + b.y), x.z + (v.z + b.z),
+                                   x.w + (v.w + b.w));
+      if constexpr (ASM)
+        st_b128_asm(p, y);
+      else
+        *p = y;
+    } else {
+      i16x4* p = (i16x4*)(X + (size_t)r * ldx + c);
+      const i16x4 x = *p;
+      i16x4 o;
+      o[0] = to_bits<R>(fin(from_bits<R>(x[0]) + (v.x + b.x)));
+      o[1] = to_bits<R>(fin(from_bits<R>(x[1]) + (v.y + b.y)));
+      o[2] = to_bits<R>(fin(from_bits<R>(x[2]) + (v.z + b.z)));
+      o[3] = to_bits<R>(fin(from_bits<R>(x[3]) + (v.w + b.w)));
+      if constexpr (ASM)
+        st_b64_asm(p, o);
+      else
+        *p = o;
+    }
   }
   MICLIP_DEV void put1(int r, int c, float v, float b) const {
-    float* p = X + (size_t)r * ldx + c;
-    *p = *p + (v + b);
+    R* p = X + (size_t)r * ldx + c;
+    if constexpr (std::is_same_v<R, float>)
+      *p = *p + (v + b);
+    else
+      *p = to_t<R>(fin((float)*p + (v + b)));
   }
 };
 
@@ -225,8 +251,9 @@ struct EpiNull {
   }
 };
 
+template <typename R>
 struct EpiPatch {
-  float* X;
+  R* X;
   const float* pos;
   int ldx;
   int np;
@@ -242,13 +269,23 @@ struct EpiPatch {
     const int p = r % np;
     const float4 q = *(const float4*)(pos + (size_t)(1 + p) * ldx + c);
     const float4 y = make_float4(v.x + q.x, v.y + q.y, v.z + q.z, v.w + q.w);
-    if constexpr (ASM)
-      st_b128_asm(X + row_of(r) * ldx + c, y);
-    else
-      *(float4*)(X + row_of(r) * ldx + c) = y;
+    if constexpr (std::is_same_v<R, float>) {
+      if constexpr (ASM)
+        st_b128_asm(X + row_of(r) * ldx + c, y);
+      else
+        *(float4*)(X + row_of(r) * ldx + c) = y;
+    } else {
+      i16x4 o;
+      o[0] = to_bits<R>(EpiResidual<R>::fin(y.x));
+      o[1] = to_bits<R>(EpiResidual<R>::fin(y.y));
+      o[2] = to_bits<R>(EpiResidual<R>::fin(y.z));
+      o[3] = to_bits<R>(EpiResidual<R>::fin(y.w));
+      *(i16x4*)(X + row_of(r) * ldx + c) = o;
+    }
   }
   MICLIP_DEV void put1(int r, int c, float v, float) const {
-    X[row_of(r) * ldx + c] = v + pos[(size_t)(1 + r % np) * ldx + c];
+    X[row_of(r) * ldx + c] =
+        to_t<R>(EpiResidual<R>::fin(v + pos[(size_t)(1 + r % np) * ldx + c]));
   }
 };
 
@@ -432,7 +469,7 @@ MICLIP_DEV void load_bias_regs(const Epi& epi, int n0, int wc, int lane, float4 
 template <bool GUARD>
 MICLIP_DEV void epilogue_residual_regs(const f32x4 (&acc)[2][2][4][2],
                                        const float4 (&bv)[2][2], int m0, int n0, int wr,
-                                       int wc, int lane, int M, const EpiResidual& epi) {
+                                       int wc, int lane, int M, const EpiResidual<float>& epi) {
   const int fk = lane >> 4, q = (lane & 15) >> 2, jj = lane & 3;
   auto row_of = [&](int k) {
     const int r = m0 + wr * 128 + (k >> 2) * 64 + (k & 3) * 16 + fk * 4 + jj;
@@ -472,7 +509,7 @@ template <bool GUARD, class Epi>
 MICLIP_DEV void epilogue_regs_body(const f32x4 (&acc)[2][2][4][2], const float4 (&bv)[2][2],
                                    int m0, int n0, int wr, int wc, int lane, int M,
                                    const Epi& epi) {
-  if constexpr (std::is_same_v<Epi, EpiResidual>) {
+  if constexpr (std::is_same_v<Epi, EpiResidual<float>>) {
     epilogue_residual_regs<GUARD>(acc, bv, m0, n0, wr, wc, lane, M, epi);
     return;
   }
@@ -968,8 +1005,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
 // retires exactly (or, capped, slightly more than) what is needed.
 // ---------------------------------------------------------------------------
 template <class Epi> struct EpiOps { static constexpr int n = 32 + 4; };   // stores + next bias
-template <> struct EpiOps<EpiResidual> { static constexpr int n = 64 + 4; };   // + x loads
-template <> struct EpiOps<EpiPatch> { static constexpr int n = 64 + 4; };      // pos loads + stores
+template <typename R> struct EpiOps<EpiResidual<R>> { static constexpr int n = 64 + 4; };  // + x loads
+template <typename R> struct EpiOps<EpiPatch<R>> { static constexpr int n = 64 + 4; };  // pos + stores
+template <class Epi> struct IsPatch : std::false_type {};
+template <typename R> struct IsPatch<EpiPatch<R>> : std::true_type {};
 
 template <typename T, class Epi>
 __global__ __launch_bounds__(512) void gemm256p_kernel(const T* __restrict__ A,
@@ -1376,7 +1415,7 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
     const int tiles = ((M + 255) / 256) * (N / 256);
     // needs >= 2 K-tiles (the stream stages at most one tile ahead); the
     // patch-embed epilogue keeps the one-tile-per-workgroup kernel
-    if (!std::is_same_v<Epi, EpiPatch> && N % 256 == 0 && K >= 128) {
+    if (!IsPatch<Epi>::value && N % 256 == 0 && K >= 128) {
       const int grid = tiles < ncu ? tiles : ncu;
       hipLaunchKernelGGL((gemm256p_kernel<T, Epi>), dim3(grid), dim3(512), 0, s, (const T*)A,
                          (const T*)W, M, N, K, epi, gm);
@@ -1455,10 +1494,15 @@ hipError_t gemm_store(int dtype, const void* A, const void* W, const float* bias
   return gemm_store_t<__bf16>(A, W, bias, C, M, N, K, act, s, v);
 }
 
-hipError_t gemm_residual(int dtype, const void* A, const void* W, const float* bias, float* X,
-                         int M, int N, int K, hipStream_t s, int v) {
-  if (dtype == kF16) return launch<_Float16>(A, W, M, N, K, EpiResidual{X, bias, N}, s, v);
-  return launch<__bf16>(A, W, M, N, K, EpiResidual{X, bias, N}, s, v);
+hipError_t gemm_residual(int dtype, const void* A, const void* W, const float* bias, void* X,
+                         int M, int N, int K, hipStream_t s, int v, int resid16) {
+  if (resid16) {  // fp16 residual stream: fp16 compute only
+    if (dtype != kF16) return hipErrorInvalidValue;
+    return launch<_Float16>(A, W, M, N, K, EpiResidual<_Float16>{(_Float16*)X, bias, N}, s, v);
+  }
+  if (dtype == kF16)
+    return launch<_Float16>(A, W, M, N, K, EpiResidual<float>{(float*)X, bias, N}, s, v);
+  return launch<__bf16>(A, W, M, N, K, EpiResidual<float>{(float*)X, bias, N}, s, v);
 }
 
 hipError_t gemm_f32(int dtype, const void* A, const void* W, const float* bias, float* C, int M,
@@ -1473,11 +1517,16 @@ hipError_t gemm_null(int dtype, const void* A, const void* W, float* C, int M, i
   return launch<__bf16>(A, W, M, N, K, EpiNull{C, 0}, s, v);
 }
 
-hipError_t gemm_patch(int dtype, const void* A, const void* W, const float* pos, float* X, int M,
-                      int N, int K, int np, hipStream_t s) {
+hipError_t gemm_patch(int dtype, const void* A, const void* W, const float* pos, void* X, int M,
+                      int N, int K, int np, hipStream_t s, int resid16) {
   if (np <= 0 || M % np) return hipErrorInvalidValue;
-  if (dtype == kF16) return launch<_Float16>(A, W, M, N, K, EpiPatch{X, pos, N, np}, s);
-  return launch<__bf16>(A, W, M, N, K, EpiPatch{X, pos, N, np}, s);
+  if (resid16) {
+    if (dtype != kF16) return hipErrorInvalidValue;
+    return launch<_Float16>(A, W, M, N, K, EpiPatch<_Float16>{(_Float16*)X, pos, N, np}, s);
+  }
+  if (dtype == kF16)
+    return launch<_Float16>(A, W, M, N, K, EpiPatch<float>{(float*)X, pos, N, np}, s);
+  return launch<__bf16>(A, W, M, N, K, EpiPatch<float>{(float*)X, pos, N, np}, s);
 }
 
 }  // namespace miclip

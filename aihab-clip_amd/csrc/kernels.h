@@ -17,9 +17,10 @@ enum Act { ACT_NONE = 0, ACT_QUICKGELU = 1, ACT_GELU = 2 };
 // `variant`: 0 = pick by size, 128 / 256 = force that tile (tests, A/B timing).
 hipError_t gemm_store(int dtype, const void* A, const void* W, const float* bias, void* C,
                       int M, int N, int K, int act, hipStream_t s, int variant = 0);
-// Residual epilogue: X (fp32, ld = N) += acc + bias.
-hipError_t gemm_residual(int dtype, const void* A, const void* W, const float* bias, float* X,
-                         int M, int N, int K, hipStream_t s, int variant = 0);
+// Residual epilogue: X (ld = N) += acc + bias; X fp32, or fp16 when resid16
+// (fp16 compute only: the reference's fp16 GPU residual stream).
+hipError_t gemm_residual(int dtype, const void* A, const void* W, const float* bias, void* X,
+                         int M, int N, int K, hipStream_t s, int variant = 0, int resid16 = 0);
 // Float epilogue: C (fp32, ld = N) = acc + bias (bias may be null).
 hipError_t gemm_f32(int dtype, const void* A, const void* W, const float* bias, float* C,
                     int M, int N, int K, hipStream_t s, int variant = 0);
@@ -27,17 +28,20 @@ hipError_t gemm_f32(int dtype, const void* A, const void* W, const float* bias, 
 hipError_t gemm_null(int dtype, const void* A, const void* W, float* C, int M, int N, int K,
                      hipStream_t s, int variant = 0);
 // Patch-embed epilogue: row m = b*np + p of the patch GEMM goes to token row
-// b*(np+1) + 1 + p of X (fp32, ld = N), plus positional embedding row 1 + p.
-hipError_t gemm_patch(int dtype, const void* A, const void* W, const float* pos, float* X,
-                      int M, int N, int K, int np, hipStream_t s);
+// b*(np+1) + 1 + p of X (fp32, or fp16 when resid16; ld = N), plus positional
+// embedding row 1 + p.
+hipError_t gemm_patch(int dtype, const void* A, const void* W, const float* pos, void* X,
+                      int M, int N, int K, int np, hipStream_t s, int resid16 = 0);
 
 // ---- LayerNorm (fp32 statistics, eps 1e-5) over rows of width D ----
-// Row r of the input is at in + in_row(r)*D with in_row(r) = rows ? rows[r] : r*in_stride_rows.
-// out_f32 != null -> fp32 output (may alias in); else out_t in compute dtype.
+// Row r of the input is at in + in_row(r)*D with in_row(r) = rows ? rows[r] : r*in_stride_rows;
+// the input is fp32, or fp16 when in16 (fp16 residual stream).
+// out_f32 != null -> fp32 output (may alias an fp32 in); else out_t in compute dtype (may
+// alias an fp16 in of the same dtype).
 // normalize != 0 additionally L2-normalises each output row (F.normalize, eps 1e-12).
-hipError_t layernorm(int dtype, const float* in, const int32_t* rows, int in_stride_rows,
+hipError_t layernorm(int dtype, const void* in, const int32_t* rows, int in_stride_rows,
                      const float* gamma, const float* beta, float* out_f32, void* out_t,
-                     int R, int D, int normalize, hipStream_t s);
+                     int R, int D, int normalize, hipStream_t s, int in16 = 0);
 
 // ---- fused multi-head attention over a packed QKV buffer ----
 // qkv: [B*N, 3*H*dh] compute dtype (torch in_proj order q|k|v); out: [B*N, H*dh].
@@ -54,13 +58,14 @@ hipError_t attention(int dtype, const void* qkv, void* out, int B, int N, int H,
 // zero-padded up to Kp (multiple of 64).
 hipError_t im2col(int dtype, const float* img, void* patches, int B, int R, int P, int Kp,
                   hipStream_t s);
-// X[b*ntok + 0, :] = cls + pos[0, :]
-hipError_t class_token(const float* cls, const float* pos, float* X, int B, int ntok, int D,
-                       hipStream_t s);
+// X[b*ntok + 0, :] = cls + pos[0, :]  (X fp32, or fp16 when resid16)
+hipError_t class_token(const float* cls, const float* pos, void* X, int B, int ntok, int D,
+                       hipStream_t s, int resid16 = 0);
 // X[p*L + t, :] = tok_emb[tokens[p*L + t], :] + pos[t, :]; eot[p] = argmax_t tokens[p*L+t]
-// as a row index p*L + argmax (first maximum, like torch.argmax).
-hipError_t token_embed(const int64_t* tokens, const float* tok_emb, const float* pos, float* X,
-                       int32_t* eot_rows, int P, int L, int D, int vocab, hipStream_t s);
+// as a row index p*L + argmax (first maximum, like torch.argmax). X fp32 / fp16 (resid16).
+hipError_t token_embed(const int64_t* tokens, const float* tok_emb, const float* pos, void* X,
+                       int32_t* eot_rows, int P, int L, int D, int vocab, hipStream_t s,
+                       int resid16 = 0);
 // out[r, :] = in[r, :] @ Wm  (fp32, Wm [D, E] row-major)
 hipError_t rowvec_matmul(const float* in, const float* Wm, float* out, int R, int D, int E,
                          hipStream_t s);

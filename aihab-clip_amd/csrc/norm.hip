@@ -15,8 +15,21 @@ namespace miclip {
 
 namespace {
 
-template <int VPL, typename T>  // VPL = float4 vectors per lane (D = 256*VPL)
-__global__ __launch_bounds__(256) void layernorm_kernel(const float* in,  // may alias out_f32
+// 4 consecutive input elements as fp32 (TI = float, or _Float16 for the fp16
+// residual stream: 8-byte loads)
+template <typename TI>
+MICLIP_DEV float4 load4(const TI* p, size_t i4) {
+  if constexpr (std::is_same_v<TI, float>) {
+    return ((const float4*)p)[i4];
+  } else {
+    const i16x4 h = ((const i16x4*)p)[i4];
+    return make_float4(from_bits<TI>(h[0]), from_bits<TI>(h[1]), from_bits<TI>(h[2]),
+                       from_bits<TI>(h[3]));
+  }
+}
+
+template <int VPL, typename T, typename TI>  // VPL = float4 vectors per lane (D = 256*VPL)
+__global__ __launch_bounds__(256) void layernorm_kernel(const TI* in,  // may alias out_f32 / out_t
                                                         const int32_t* __restrict__ rows,
                                                         int in_stride_rows,
                                                         const float* __restrict__ gamma,
@@ -27,12 +40,12 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* in,  // may
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= R) return;
   const size_t src_row = rows ? (size_t)rows[r] : (size_t)r * in_stride_rows;
-  const float4* src = (const float4*)(in + src_row * D);
+  const TI* src = in + src_row * D;
   float4 v[VPL];
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
-    v[i] = src[i * 64 + lane];
+    v[i] = load4<TI>(src, i * 64 + lane);
     s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
   }
   const float mean = wave_sum(s) / (float)D;
@@ -80,14 +93,14 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* in,  // may
   }
 }
 
-template <typename T>
-hipError_t ln_dispatch(const float* in, const int32_t* rows, int stride, const float* g,
+template <typename T, typename TI>
+hipError_t ln_dispatch(const TI* in, const int32_t* rows, int stride, const float* g,
                        const float* b, float* of, void* ot, int R, int D, int nz, hipStream_t s) {
   const dim3 grid((R + 3) / 4), block(256);
-#define MICLIP_LN_CASE(V)                                                                   \
-  case V:                                                                                   \
-    hipLaunchKernelGGL((layernorm_kernel<V, T>), grid, block, 0, s, in, rows, stride, g, b, \
-                       of, (T*)ot, R, D, nz);                                               \
+#define MICLIP_LN_CASE(V)                                                                       \
+  case V:                                                                                       \
+    hipLaunchKernelGGL((layernorm_kernel<V, T, TI>), grid, block, 0, s, in, rows, stride, g, b, \
+                       of, (T*)ot, R, D, nz);                                                   \
     break;
   switch (D / 256) {
     MICLIP_LN_CASE(1)
@@ -105,15 +118,20 @@ hipError_t ln_dispatch(const float* in, const int32_t* rows, int stride, const f
 
 }  // namespace
 
-hipError_t layernorm(int dtype, const float* in, const int32_t* rows, int in_stride_rows,
+hipError_t layernorm(int dtype, const void* in, const int32_t* rows, int in_stride_rows,
                      const float* gamma, const float* beta, float* out_f32, void* out_t, int R,
-                     int D, int normalize, hipStream_t s) {
+                     int D, int normalize, hipStream_t s, int in16) {
   if (R < 1 || D % 256 || D > 1536 || (!out_f32 && !out_t)) return hipErrorInvalidValue;
+  if (in16) {  // fp16 residual stream: fp16 compute only
+    if (dtype != kF16) return hipErrorInvalidValue;
+    return ln_dispatch<_Float16>((const _Float16*)in, rows, in_stride_rows, gamma, beta, out_f32,
+                                 out_t, R, D, normalize, s);
+  }
   if (dtype == kF16)
-    return ln_dispatch<_Float16>(in, rows, in_stride_rows, gamma, beta, out_f32, out_t, R, D,
-                                 normalize, s);
-  return ln_dispatch<__bf16>(in, rows, in_stride_rows, gamma, beta, out_f32, out_t, R, D,
-                             normalize, s);
+    return ln_dispatch<_Float16>((const float*)in, rows, in_stride_rows, gamma, beta, out_f32,
+                                 out_t, R, D, normalize, s);
+  return ln_dispatch<__bf16>((const float*)in, rows, in_stride_rows, gamma, beta, out_f32, out_t,
+                             R, D, normalize, s);
 }
 
 }  // namespace miclip

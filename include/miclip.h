@@ -199,17 +199,20 @@ int miclip_profile_read(miclip_model* m, miclip_kernel_stat* out, int32_t n, int
 
 /* C = A[M,K] . W[N,K]^T + bias, A/W in compute dtype `dtype`.
  * epi 0: C dtype = act(.) with act from `act` (0 none); epi 1: C fp32 += (residual);
- * epi 2: C fp32 = . ; epi 3: no output (diagnostic: prices the epilogue); N % 128 == 0 and K % 64 == 0 required. variant: 0 = tile
+ * epi 2: C fp32 = . ; epi 3: no output (diagnostic: prices the epilogue);
+ * epi 4: C fp16 += . (fp16 residual stream; dtype MICLIP_FP16 only).
+ * N % 128 == 0 and K % 64 == 0 required. variant: 0 = tile
  * chosen by size, 128 / 256 = force the 128x128 / 256x256 kernel (N % 256 for 256).
  * Replaces torch Linear (clip/model.py:171-175) and MHA in/out projections. */
 int miclip_op_gemm(int32_t dtype, const void* A, const void* W, const float* bias, void* C,
                    int32_t M, int32_t N, int32_t K, int32_t epi, int32_t act, int32_t variant,
                    void* stream);
 
-/* LayerNorm over R rows of width D (fp32 in, eps 1e-5), out in fp32 (out_is_f32)
- * or compute dtype; replaces the reference LayerNorm (clip/model.py:151-157). */
-int miclip_op_layernorm(int32_t dtype, const float* in, const float* gamma, const float* beta,
-                        void* out, int32_t out_is_f32, int32_t R, int32_t D, void* stream);
+/* LayerNorm over R rows of width D (eps 1e-5, fp32 statistics); replaces the
+ * reference LayerNorm (clip/model.py:151-157). flags bit 0: out fp32 (else compute
+ * dtype); bit 1: in fp16 (the fp16 residual stream; dtype MICLIP_FP16 only), else fp32. */
+int miclip_op_layernorm(int32_t dtype, const void* in, const float* gamma, const float* beta,
+                        void* out, int32_t flags, int32_t R, int32_t D, void* stream);
 
 /* softmax(Q K^T / sqrt(dh) + mask) V per head over a packed qkv [B*N, 3*H*dh]
  * buffer, out [B*N, H*dh]; replaces F.scaled_dot_product_attention inside

@@ -43,7 +43,7 @@ def _check(lib, rc):
                                           (4096, 1024, 1024, 258), (33, 2304, 128, 258),
                                           (1000, 768, 3072, 260), (300, 256, 192, 260), (257, 512, 64, 260),
                                           (4096, 1024, 1024, 260), (33, 2304, 128, 260)])
-@pytest.mark.parametrize("epi,act", [(0, 0), (0, 1), (0, 2), (1, 0), (2, 0)])
+@pytest.mark.parametrize("epi,act", [(0, 0), (0, 1), (0, 2), (1, 0), (2, 0), (4, 0)])
 def test_gemm(lib, dt, M, N, K, variant, epi, act):
     code, tdt = DT[dt]
     g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K + epi * 3 + act)
@@ -61,13 +61,22 @@ def test_gemm(lib, dt, M, N, K, variant, epi, act):
         X0 = torch.randn(M, N, device="cuda", generator=g)
         C = X0.clone()
         ref = X0 + ref
+    elif epi == 4:   # fp16 residual stream (fp16 compute only)
+        if dt != "fp16":
+            assert lib.miclip_op_gemm(code, A.data_ptr(), W.data_ptr(), bias.data_ptr(), A.data_ptr(),
+                                      M, N, K, epi, act, variant, _stream()) != 0
+            return
+        X0 = torch.randn(M, N, device="cuda", generator=g).half()
+        C = X0.clone()
+        ref = X0.float() + ref
     else:
         C = torch.empty(M, N, device="cuda", dtype=torch.float32)
     _check(lib, lib.miclip_op_gemm(code, A.data_ptr(), W.data_ptr(), bias.data_ptr(), C.data_ptr(),
                                    M, N, K, epi, act, variant, _stream()))
     torch.cuda.synchronize()
     err = (C.float() - ref).abs().max().item()
-    tol = (2e-2 if dt == "bf16" else 4e-3) * max(1.0, ref.abs().max().item()) if epi == 0 else 2e-4 * K ** 0.5
+    tol = ((2e-2 if dt == "bf16" else 4e-3) * max(1.0, ref.abs().max().item()) if epi in (0, 4)
+           else 2e-4 * K ** 0.5)
     assert err <= tol, f"max|err| {err} > {tol}"
 
 
@@ -79,7 +88,7 @@ NO_TAIL = 1 << 16   # gemm.hip kGemmNoTail: every row in 256x256 tiles
                                    (16448, 3072, 256), (16500, 1024, 2048), (4352, 4096, 512),
                                    (4296, 4096, 256), (16640, 3072, 256)])
 @pytest.mark.parametrize("variant", [258, 260, 256, 258 | (1 << 17), 260 | (1 << 17)])
-@pytest.mark.parametrize("epi,act", [(0, 0), (0, 1), (0, 2), (1, 0), (2, 0)])
+@pytest.mark.parametrize("epi,act", [(0, 0), (0, 1), (0, 2), (1, 0), (2, 0), (4, 0)])
 def test_gemm_tail_bitexact(lib, dt, M, N, K, variant, epi, act):
     """Row tail of a 256x256 launch (rows past the last whole round of tiles,
     computed as 16-row slivers of tiles (SCHED 2) or by tail workgroups) equals the all-tile launch bit for bit
@@ -93,6 +102,11 @@ def test_gemm_tail_bitexact(lib, dt, M, N, K, variant, epi, act):
         mk = lambda: torch.empty(M, N, device="cuda", dtype=tdt)  # noqa: E731
     elif epi == 1:
         X0 = torch.randn(M, N, device="cuda", generator=g)
+        mk = X0.clone
+    elif epi == 4:
+        if dt != "fp16":
+            pytest.skip("fp16 residual stream runs with fp16 compute only")
+        X0 = torch.randn(M, N, device="cuda", generator=g).half()
         mk = X0.clone
     else:
         mk = lambda: torch.empty(M, N, device="cuda", dtype=torch.float32)  # noqa: E731
@@ -109,10 +123,11 @@ def test_gemm_tail_bitexact(lib, dt, M, N, K, variant, epi, act):
         ref = ref * torch.sigmoid(1.702 * ref)
     if epi == 0 and act == 2:
         ref = torch.nn.functional.gelu(ref)
-    if epi == 1:
-        ref = X0[-300:] + ref
+    if epi in (1, 4):
+        ref = X0[-300:].float() + ref
     err = (outs[0][-300:].float() - ref).abs().max().item()
-    tol = (2e-2 if dt == "bf16" else 4e-3) * max(1.0, ref.abs().max().item()) if epi == 0 else 2e-4 * K ** 0.5
+    tol = ((2e-2 if dt == "bf16" else 4e-3) * max(1.0, ref.abs().max().item()) if epi in (0, 4)
+           else 2e-4 * K ** 0.5)
     assert err <= tol, f"max|err| {err} > {tol}"
 
 
@@ -146,6 +161,31 @@ def test_layernorm(lib, dt, R, D):
     torch.cuda.synchronize()
     assert (out32 - ref).abs().max().item() < 1e-4
     assert (outt.float() - ref).abs().max().item() < (3e-2 if dt == "bf16" else 4e-3)
+
+
+@pytest.mark.parametrize("R,D", [(7, 768), (513, 1024), (3, 1280), (300, 1536)])
+def test_layernorm_fp16_stream(lib, R, D):
+    """fp16 input (the fp16 residual stream): fp32 out, fp16 out, and fp16 in place (ln_pre)."""
+    x = (torch.randn(R, D, device="cuda") * 3 + 0.5).half()
+    gam = 1 + 0.1 * torch.randn(D, device="cuda")
+    bet = 0.05 * torch.randn(D, device="cuda")
+    ref = torch.nn.functional.layer_norm(x.float(), (D,), gam, bet, 1e-5)
+    out32 = torch.empty(R, D, device="cuda")
+    _check(lib, lib.miclip_op_layernorm(0, x.data_ptr(), gam.data_ptr(), bet.data_ptr(),
+                                        out32.data_ptr(), 1 | 2, R, D, _stream()))
+    out16 = torch.empty(R, D, device="cuda", dtype=torch.float16)
+    _check(lib, lib.miclip_op_layernorm(0, x.data_ptr(), gam.data_ptr(), bet.data_ptr(),
+                                        out16.data_ptr(), 2, R, D, _stream()))
+    xin = x.clone()
+    _check(lib, lib.miclip_op_layernorm(0, xin.data_ptr(), gam.data_ptr(), bet.data_ptr(),
+                                        xin.data_ptr(), 2, R, D, _stream()))
+    torch.cuda.synchronize()
+    assert (out32 - ref).abs().max().item() < 1e-4
+    assert (out16.float() - ref).abs().max().item() < 4e-3
+    assert torch.equal(xin, out16)
+    # bf16 compute with an fp16 stream is refused
+    assert lib.miclip_op_layernorm(1, x.data_ptr(), gam.data_ptr(), bet.data_ptr(),
+                                   out16.data_ptr(), 2, R, D, _stream()) != 0
 
 
 def _attn_ref(qkv, B, N, H, causal, dh=64):

@@ -68,6 +68,26 @@ def test_encode_image_matches_reference(golden, tag, name, dtype):
     assert d.max() <= COS_TOL
 
 
+def test_fp32_residual_stream_option(golden, monkeypatch):
+    """MICLIP_RESID_F32=1 keeps an fp32 residual stream under fp16 compute (the
+    default streams fp16 like the reference's GPU model); both meet the tolerance."""
+    import miclip
+    from miclip.weights import synthetic_images
+    g = golden("vitb16")
+    imgs = torch.from_numpy(synthetic_images(g["meta"]["n_images"], 224, seed=0)).cuda()
+    _models.clear()
+    monkeypatch.setenv("MICLIP_RESID_F32", "1")
+    _, m32, _ = miclip.load("ViT-B/16", device="cuda", compute_dtype="fp16")
+    f32 = m32.encode_image(imgs).cpu()
+    del m32
+    monkeypatch.delenv("MICLIP_RESID_F32")
+    f16 = _model("ViT-B/16", "fp16").encode_image(imgs).cpu()
+    d32, d16 = _one_minus_cos(f32, g["image"]), _one_minus_cos(f16, g["image"])
+    print(f"vitb16: 1-cos fp32 stream {d32.max():.2e}, fp16 stream {d16.max():.2e}")
+    assert d32.max() <= COS_TOL and d16.max() <= COS_TOL
+    assert not torch.equal(f32, f16), "the option did not change the stream"
+
+
 @pytest.mark.parametrize("dtype", ["fp16", "bf16"])
 @pytest.mark.parametrize("tag,name", CONFIGS[:3] + CONFIGS[4:])
 def test_encode_text_matches_reference(golden, tag, name, dtype):
