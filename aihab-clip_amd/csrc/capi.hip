@@ -76,6 +76,8 @@ struct Block {
   void* w_proj = nullptr;
   float* b_proj = nullptr;
   float *ln1_g = nullptr, *ln1_b = nullptr, *ln2_g = nullptr, *ln2_b = nullptr;
+  // MX-fp8 models: scale planes of w_qkv / w_fc / w_proj (which then hold e4m3 bytes)
+  void *s_qkv = nullptr, *s_fc = nullptr, *s_proj = nullptr;
 };
 
 struct Workspace {
@@ -87,6 +89,8 @@ struct Workspace {
   void* qkv = nullptr;
   void* o = nullptr;
   void* f = nullptr;
+  // MX-fp8 models: LayerNorm output (hq, scales hs) and c_fc output (fq, fs)
+  void *hq = nullptr, *hs = nullptr, *fq = nullptr, *fs = nullptr;
   float* feat = nullptr;  // [items, W] fp32 scratch
   int32_t* rows = nullptr;
 };
@@ -102,6 +106,9 @@ struct miclip_model {
   // activations of VisionTransformer / Transformer). Default with fp16 compute;
   // MICLIP_RESID_F32=1 keeps an fp32 stream. bf16 compute always streams fp32.
   int resid16 = 0;
+  // MICLIP_MXFP8: QKV / c_fc / c_proj run on MX-fp8 operands (gemm_mx.hip);
+  // everything else (patch embed, attention, out-proj, stream) as fp16 compute.
+  bool mx = false;
   int Kp = 0;  // padded patch-GEMM K
   std::unordered_map<void*, size_t> allocs;
   int64_t bytes = 0;
@@ -112,6 +119,7 @@ struct miclip_model {
     int kind;  // 0 = fp32 as-is, 1 = GEMM weight in compute dtype, 2 = conv1 -> [W, Kp]
     bool loaded;
     bool visual;
+    void** sdst = nullptr;  // MX-fp8 weight: its scale plane (dst then holds e4m3 bytes)
   };
   std::unordered_map<std::string, Slot> slots;
   std::vector<Block> vblocks, tblocks;
@@ -188,20 +196,23 @@ struct ProfScope {
 int elt() { return 2; }
 
 void add_slot(miclip_model* m, const std::string& name, void** dst, int64_t numel, int kind,
-              bool visual) {
-  m->slots[name] = miclip_model::Slot{dst, numel, kind, false, visual};
+              bool visual, void** sdst = nullptr) {
+  m->slots[name] = miclip_model::Slot{dst, numel, kind, false, visual, sdst};
 }
 
 void add_block_slots(miclip_model* m, const std::string& prefix, Block& b, int W, bool visual) {
-  add_slot(m, prefix + "attn.in_proj_weight", &b.w_qkv, (int64_t)3 * W * W, 1, visual);
+  add_slot(m, prefix + "attn.in_proj_weight", &b.w_qkv, (int64_t)3 * W * W, 1, visual,
+           m->mx ? &b.s_qkv : nullptr);
   add_slot(m, prefix + "attn.in_proj_bias", (void**)&b.b_qkv, 3 * W, 0, visual);
   add_slot(m, prefix + "attn.out_proj.weight", &b.w_out, (int64_t)W * W, 1, visual);
   add_slot(m, prefix + "attn.out_proj.bias", (void**)&b.b_out, W, 0, visual);
   add_slot(m, prefix + "ln_1.weight", (void**)&b.ln1_g, W, 0, visual);
   add_slot(m, prefix + "ln_1.bias", (void**)&b.ln1_b, W, 0, visual);
-  add_slot(m, prefix + "mlp.c_fc.weight", &b.w_fc, (int64_t)4 * W * W, 1, visual);
+  add_slot(m, prefix + "mlp.c_fc.weight", &b.w_fc, (int64_t)4 * W * W, 1, visual,
+           m->mx ? &b.s_fc : nullptr);
   add_slot(m, prefix + "mlp.c_fc.bias", (void**)&b.b_fc, 4 * W, 0, visual);
-  add_slot(m, prefix + "mlp.c_proj.weight", &b.w_proj, (int64_t)4 * W * W, 1, visual);
+  add_slot(m, prefix + "mlp.c_proj.weight", &b.w_proj, (int64_t)4 * W * W, 1, visual,
+           m->mx ? &b.s_proj : nullptr);
   add_slot(m, prefix + "mlp.c_proj.bias", (void**)&b.b_proj, W, 0, visual);
   add_slot(m, prefix + "ln_2.weight", (void**)&b.ln2_g, W, 0, visual);
   add_slot(m, prefix + "ln_2.bias", (void**)&b.ln2_b, W, 0, visual);
@@ -244,7 +255,8 @@ int ensure_ws(miclip_model* m, Workspace& w, int items, int ntok, int W, bool im
   const size_t e = elt();
   // grow: make sure no queued kernel still uses the old buffers
   MICLIP_HIP(hipDeviceSynchronize());
-  for (void* p : {w.patches, (void*)w.x, w.h, w.qkv, w.o, w.f, (void*)w.feat, (void*)w.rows})
+  for (void* p : {w.patches, (void*)w.x, w.h, w.qkv, w.o, w.f, w.hq, w.hs, w.fq, w.fs,
+                  (void*)w.feat, (void*)w.rows})
     dev_free(m, p);
   w = Workspace{};
   int rc;
@@ -257,6 +269,14 @@ int ensure_ws(miclip_model* m, Workspace& w, int items, int ntok, int W, bool im
   if ((rc = dev_alloc(m, &w.qkv, (size_t)rows * 3 * W * e))) return rc;
   if ((rc = dev_alloc(m, &w.o, (size_t)rows * W * e))) return rc;
   if ((rc = dev_alloc(m, &w.f, (size_t)rows * 4 * W * e))) return rc;
+  if (m->mx) {
+    // scale planes: + 4 blocks of 256 rows so that every batch-split window
+    // (view) starts on its own 256-row block
+    if ((rc = dev_alloc(m, &w.hq, (size_t)rows * W))) return rc;
+    if ((rc = dev_alloc(m, &w.hs, mx_scale_bytes(rows + 4 * 256, W)))) return rc;
+    if ((rc = dev_alloc(m, &w.fq, (size_t)rows * 4 * W))) return rc;
+    if ((rc = dev_alloc(m, &w.fs, mx_scale_bytes(rows + 4 * 256, 4 * W)))) return rc;
+  }
   if ((rc = dev_alloc(m, (void**)&w.feat, (size_t)items * W * 4))) return rc;
   if ((rc = dev_alloc(m, (void**)&w.rows, (size_t)items * 4))) return rc;
   w.cap_items = items;
@@ -275,14 +295,23 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
               int dh, int causal, hipStream_t s) {
   const int M = items * N, dt = m->dtype, r16 = m->resid16;
   const double dM = M, dW = W, rb = r16 ? 2 : 4;  // residual bytes per element
+  const bool mx = m->mx;   // MX-fp8 operands for QKV / c_fc / c_proj
   {
-    ProfScope p(m, K_LAYERNORM, s, 0, dM * dW * (rb + 2));
-    MICLIP_HIP(
-        layernorm(dt, w.x, nullptr, 1, b.ln1_g, b.ln1_b, nullptr, w.h, M, W, 0, s, r16));
+    ProfScope p(m, K_LAYERNORM, s, 0, dM * dW * (rb + (mx ? 1 : 2)));
+    if (mx)
+      MICLIP_HIP(layernorm(dt, w.x, nullptr, 1, b.ln1_g, b.ln1_b, nullptr, nullptr, M, W, 0, s,
+                           r16, w.hq, w.hs));
+    else
+      MICLIP_HIP(
+          layernorm(dt, w.x, nullptr, 1, b.ln1_g, b.ln1_b, nullptr, w.h, M, W, 0, s, r16));
   }
   {
     ProfScope p(m, K_GEMM_QKV, s, gemm_flops(dM, 3 * dW, dW), gemm_bytes(dM, 3 * dW, dW, 2));
-    MICLIP_HIP(gemm_store(dt, w.h, b.w_qkv, b.b_qkv, w.qkv, M, 3 * W, W, ACT_NONE, s));
+    if (mx)
+      MICLIP_HIP(gemm_mx(w.hq, w.hs, b.w_qkv, b.s_qkv, b.b_qkv, w.qkv, nullptr, M, 3 * W, W, 0,
+                         ACT_NONE, s));
+    else
+      MICLIP_HIP(gemm_store(dt, w.h, b.w_qkv, b.b_qkv, w.qkv, M, 3 * W, W, ACT_NONE, s));
   }
   {
     const double n = N;
@@ -294,25 +323,39 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
     MICLIP_HIP(gemm_residual(dt, w.o, b.w_out, b.b_out, w.x, M, W, W, s, 0, r16));
   }
   {
-    ProfScope p(m, K_LAYERNORM, s, 0, dM * dW * (rb + 2));
-    MICLIP_HIP(
-        layernorm(dt, w.x, nullptr, 1, b.ln2_g, b.ln2_b, nullptr, w.h, M, W, 0, s, r16));
+    ProfScope p(m, K_LAYERNORM, s, 0, dM * dW * (rb + (mx ? 1 : 2)));
+    if (mx)
+      MICLIP_HIP(layernorm(dt, w.x, nullptr, 1, b.ln2_g, b.ln2_b, nullptr, nullptr, M, W, 0, s,
+                           r16, w.hq, w.hs));
+    else
+      MICLIP_HIP(
+          layernorm(dt, w.x, nullptr, 1, b.ln2_g, b.ln2_b, nullptr, w.h, M, W, 0, s, r16));
   }
   {
-    ProfScope p(m, K_GEMM_FC, s, gemm_flops(dM, 4 * dW, dW), gemm_bytes(dM, 4 * dW, dW, 2));
-    MICLIP_HIP(gemm_store(dt, w.h, b.w_fc, b.b_fc, w.f, M, 4 * W, W, m->cfg.act, s));
+    ProfScope p(m, K_GEMM_FC, s, gemm_flops(dM, 4 * dW, dW),
+                mx ? dM * dW + 4 * dW * dW + 4 * dM * dW : gemm_bytes(dM, 4 * dW, dW, 2));
+    if (mx)
+      MICLIP_HIP(gemm_mx(w.hq, w.hs, b.w_fc, b.s_fc, b.b_fc, w.fq, w.fs, M, 4 * W, W, 5,
+                         m->cfg.act, s));
+    else
+      MICLIP_HIP(gemm_store(dt, w.h, b.w_fc, b.b_fc, w.f, M, 4 * W, W, m->cfg.act, s));
   }
   {
     ProfScope p(m, K_GEMM_PROJ, s, gemm_flops(dM, dW, 4 * dW),
-                gemm_bytes(dM, dW, 4 * dW, 2 * rb));
-    MICLIP_HIP(gemm_residual(dt, w.f, b.w_proj, b.b_proj, w.x, M, W, 4 * W, s, 0, r16));
+                mx ? 4 * dM * dW + 4 * dW * dW + 2 * rb * dM * dW
+                   : gemm_bytes(dM, dW, 4 * dW, 2 * rb));
+    if (mx)
+      MICLIP_HIP(gemm_mx(w.fq, w.fs, b.w_proj, b.s_proj, b.b_proj, w.x, nullptr, M, W, 4 * W, 1,
+                         ACT_NONE, s));
+    else
+      MICLIP_HIP(gemm_residual(dt, w.f, b.w_proj, b.b_proj, w.x, M, W, 4 * W, s, 0, r16));
   }
   return 0;
 }
 
 // A window of the workspace: rows [row0, ...) / items [item0, ...).
 Workspace view(const miclip_model* m, const Workspace& w, size_t row0, size_t item0, int N,
-               int W) {
+               int W, int part = 0) {
   Workspace v = w;
   const size_t e = elt();
   const int g = m->cfg.image_resolution / m->cfg.vision_patch_size;
@@ -322,6 +365,15 @@ Workspace view(const miclip_model* m, const Workspace& w, size_t row0, size_t it
   v.qkv = (char*)w.qkv + row0 * 3 * W * e;
   v.o = (char*)w.o + row0 * W * e;
   v.f = (char*)w.f + row0 * 4 * W * e;
+  if (w.hq) {
+    // window `part` starts its scale planes at 256-row block ceil(row0/256) + part:
+    // ceil(a) + ceil(b) <= ceil(a + b) + 1, so windows never share a block
+    const size_t blk = (row0 + 255) / 256 + part;
+    v.hq = (char*)w.hq + row0 * W;
+    v.fq = (char*)w.fq + row0 * 4 * W;
+    v.hs = (char*)w.hs + blk * (W / 128) * 1024;
+    v.fs = (char*)w.fs + blk * (4 * W / 128) * 1024;
+  }
   v.feat = w.feat + item0 * W;
   v.rows = w.rows + item0;
   (void)N;
@@ -404,8 +456,12 @@ bool cfg_ok(const miclip_config& c, std::string& why) {
   if (c.context_length < 1 || c.context_length > 640) return bad("context_length out of range");
   if (c.vision_layers < 1 || c.transformer_layers < 0) return bad("bad layer count");
   if (c.embed_dim < 1 || c.vocab_size < 1) return bad("bad embed_dim / vocab_size");
-  if (c.compute_dtype != MICLIP_FP16 && c.compute_dtype != MICLIP_BF16)
-    return bad("compute_dtype must be MICLIP_FP16 or MICLIP_BF16");
+  if (c.compute_dtype != MICLIP_FP16 && c.compute_dtype != MICLIP_BF16 &&
+      c.compute_dtype != MICLIP_MXFP8)
+    return bad("compute_dtype must be MICLIP_FP16, MICLIP_BF16 or MICLIP_MXFP8");
+  if (c.compute_dtype == MICLIP_MXFP8 &&
+      (c.vision_width % 256 || c.transformer_width % 256))
+    return bad("MICLIP_MXFP8 needs widths that are multiples of 256");
   if (c.act != MICLIP_ACT_QUICKGELU && c.act != MICLIP_ACT_GELU) return bad("bad act");
   return true;
 }
@@ -430,10 +486,11 @@ int miclip_model_create(const miclip_config* cfg, int device, miclip_model** out
   auto* m = new miclip_model();
   m->cfg = c;
   m->device = device;
-  m->dtype = cfg->compute_dtype;
+  m->mx = cfg->compute_dtype == MICLIP_MXFP8;
+  m->dtype = m->mx ? MICLIP_FP16 : cfg->compute_dtype;   // the fp16 kernels' operand type
   {
     const char* e = getenv("MICLIP_RESID_F32");
-    m->resid16 = m->dtype == MICLIP_FP16 && !(e && atoi(e) != 0);
+    m->resid16 = m->mx || (m->dtype == MICLIP_FP16 && !(e && atoi(e) != 0));
   }
   const int P = cfg->vision_patch_size, Wv = cfg->vision_width, Wt = cfg->transformer_width;
   m->Kp = (3 * P * P + 63) / 64 * 64;
@@ -500,6 +557,20 @@ int miclip_model_load_weights(miclip_model* m, const miclip_tensor* t, int32_t n
         src_cols = 3 * P * P;
         cols = m->Kp;
       }
+      if (slot.sdst) {
+        // MX-fp8 weight: fp32 rows quantised on the device (quant_mx, gemm_mx.hip)
+        const size_t nb = (size_t)rows * cols;
+        if (!*slot.dst && (rc = dev_alloc(m, slot.dst, nb))) return rc;
+        if (!*slot.sdst && (rc = dev_alloc(m, slot.sdst, mx_scale_bytes(rows, cols)))) return rc;
+        void* stage = nullptr;
+        if ((rc = dev_alloc(m, &stage, nb * 4))) return rc;
+        MICLIP_HIP(hipMemcpy(stage, t[i].data, nb * 4, hipMemcpyHostToDevice));
+        MICLIP_HIP(quant_mx(0, stage, (int)rows, (int)cols, *slot.dst, *slot.sdst, nullptr));
+        MICLIP_HIP(hipDeviceSynchronize());
+        dev_free(m, stage);
+        slot.loaded = true;
+        continue;
+      }
       tmp.assign((size_t)rows * cols, 0);
       for (int64_t r = 0; r < rows; ++r)
         for (int64_t c = 0; c < src_cols; ++c) {
@@ -555,7 +626,7 @@ int miclip_encode_image(miclip_model* m, const float* images, int32_t B, float* 
     const int nb = (B - b0) / (splits - p);
     hipStream_t sp = p == 0 ? s : m->aux[p - 1];
     if (p > 0) MICLIP_HIP(hipStreamWaitEvent(sp, m->ev_fork, 0));
-    if ((rc = encode_image_part(m, view(m, m->wimg, (size_t)b0 * N, b0, N, W),
+    if ((rc = encode_image_part(m, view(m, m->wimg, (size_t)b0 * N, b0, N, W, p),
                                 images + (size_t)b0 * 3 * R * R, nb, out + (size_t)b0 * dim,
                                 flags, sp)))
       return rc;
@@ -759,6 +830,33 @@ int miclip_op_attention(int32_t dtype, const void* qkv, void* out, int32_t B, in
   if (head_dim == 0) head_dim = 64;
   if (head_dim != 64 && head_dim != 80) return fail(MICLIP_EINVAL, "head_dim must be 64 or 80");
   MICLIP_HIP(attention(dtype, qkv, out, B, N, H, causal, (hipStream_t)stream, variant, head_dim));
+  return 0;
+}
+
+int64_t miclip_mx_scale_bytes(int32_t rows, int32_t K) {
+  return rows < 1 || K < 128 ? 0 : (int64_t)mx_scale_bytes(rows, K);
+}
+
+int miclip_op_quant_mx(const void* in, int32_t in_f16, int32_t R, int32_t K, void* q, void* scales,
+                       void* stream) {
+  if (!in || !q || !scales) return fail(MICLIP_EINVAL, "null argument");
+  MICLIP_HIP(quant_mx(in_f16, in, R, K, q, scales, (hipStream_t)stream));
+  return 0;
+}
+
+int miclip_op_gemm_mx(const void* A, const void* SA, const void* W, const void* SW,
+                      const float* bias, void* C, void* CS, int32_t M, int32_t N, int32_t K,
+                      int32_t epi, int32_t act, void* stream) {
+  if (!A || !SA || !W || !SW || !C) return fail(MICLIP_EINVAL, "null argument");
+  MICLIP_HIP(gemm_mx(A, SA, W, SW, bias, C, CS, M, N, K, epi, act, (hipStream_t)stream));
+  return 0;
+}
+
+int miclip_op_layernorm_mx(const void* in, int32_t in_f16, const float* gamma, const float* beta,
+                           void* q, void* scales, int32_t R, int32_t D, void* stream) {
+  if (!in || !gamma || !beta || !q || !scales) return fail(MICLIP_EINVAL, "null argument");
+  MICLIP_HIP(layernorm(MICLIP_FP16, in, nullptr, 1, gamma, beta, nullptr, nullptr, R, D, 0,
+                       (hipStream_t)stream, in_f16, q, scales));
   return 0;
 }
 

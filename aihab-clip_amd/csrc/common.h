@@ -21,6 +21,15 @@ typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef short i16x8 __attribute__((ext_vector_type(8)));
 typedef short i16x4_vs __attribute__((__vector_size__(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// Tiled MX scale planes (gemm_mx.hip): E8M0 byte of (row r, 32-k block kb) of an
+// operand with KT = K / 128 K-tiles -- per (256-row block, K-tile) one 1-KiB block
+// [kb & 3][r & 15][(r >> 4) & 15], the order the fp8 GEMM's lanes read.
+__host__ __device__ inline size_t mx_scale_index(int r, int kb, int KT) {
+  return ((size_t)(r >> 8) * KT + (kb >> 2)) * 1024 + (kb & 3) * 256 + (r & 15) * 16 +
+         ((r >> 4) & 15);
+}
 
 #define LDS_AS __attribute__((address_space(3)))
 #define GLB_AS __attribute__((address_space(1)))

@@ -1,0 +1,270 @@
+// GEMM epilogue functors and their helpers, shared by the f16/bf16 GEMMs
+// (gemm.hip) and the MX-fp8 GEMM (gemm_mx.hip). Internal to the library.
+#pragma once
+#include "common.h"
+#include "kernels.h"
+
+#include <type_traits>
+
+namespace miclip {
+
+namespace {
+
+// Stores issued from inline asm are invisible to hipcc's waitcnt pass. The
+// register epilogue of the persistent GEMM uses them: a compiler-visible store
+// inside the K-tile loop makes hipcc wait vmcnt(0) at the loop header (before
+// the next K-tile's ds_reads reuse the data registers), which would drain the
+// next tile's in-flight LDS-DMA every K-tile. `s_nop 1` closes the statement so
+// the data registers are read before anything overwrites them.
+MICLIP_DEV void st_b64_asm(void* p, i16x4 v) {
+  asm volatile("global_store_dwordx2 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+MICLIP_DEV void st_b128_asm(void* p, float4 v) {
+  const f32x4 w = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
+}
+
+// Epilogue functors. The kernels hoist the per-column bias load (`bias4` /
+// `bias1`, once per column a thread owns) and then call `put4` (4 consecutive
+// columns of one row, 16-B aligned) or `put1` with the raw fp32 accumulator.
+MICLIP_DEV float4 ld_bias4(const float* b, int col) {
+  return b ? *(const float4*)(b + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// Branch-free form for the register epilogue: a null bias becomes a buffer
+// descriptor with zero records, whose loads return 0 (a `b ? load : 0` select
+// makes hipcc branch around the load and wait vmcnt(0) at the join).
+MICLIP_DEV float4 ld_bias4_nb(const float* b, int col) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)b, (short)0, b ? 0x7fffffff : 0, 0x00020000);
+  const f32x4 v = __builtin_bit_cast(
+      f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)col * 4u, 0, 0));
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+
+// Exact GELU, 0.5 v erfc(-v/sqrt2), for the open_clip ViT-H/14 MLP (nn.GELU).
+// erfc from the Chebyshev fit of Numerical Recipes' erfcc (fractional error
+// < 1.2e-7 over the whole line), rewritten for the hardware: base-2 exponent
+// (v_exp_f32) with log2(e) folded into the coefficients, the 0.5 folded into
+// the exponent, and erfc(-z) = 2 - erfc(z) for v >= 0. 19 VALU ops against
+// ~40 for libm erff, and no 1 + erf cancellation in the negative tail (CPU
+// check: max abs error 2.4e-7, max rel 5e-6 against double erfc on [-12, 12]).
+// Every step is an explicit mul / fma so the scalar and the packed form
+// below round identically (the tile and tail paths must agree bit for bit).
+namespace gelu_nr {
+constexpr float L = 1.4426950408889634f;
+constexpr float kT = 0.35355339059327373f;  // 0.5 / sqrt(2): t = 1 / (1 + z/2)
+constexpr float kC[10] = {0.17087277f * L,  -0.82215223f * L, 1.48851587f * L,
+                          -1.13520398f * L, 0.27886807f * L,  -0.18628806f * L,
+                          0.09678418f * L,  0.37409196f * L,  1.00002368f * L,
+                          -1.26551223f * L - 1.0f};
+constexpr float kQ = -0.5f * L;              // -z^2 log2(e) = v^2 * kQ
+}  // namespace gelu_nr
+
+MICLIP_DEV float gelu_erf(float v) {
+  using namespace gelu_nr;
+  const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(__builtin_fabsf(v), kT, 1.0f));
+  float p = kC[0];
+#pragma unroll
+  for (int i = 1; i < 10; ++i) p = __builtin_fmaf(t, p, kC[i]);
+  const float vt = v * t;
+  const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(v * v, kQ, p));
+  const float hv = vt * e;                         // 0.5 v erfc(|v|/sqrt2)
+  const float pos = __builtin_fmaf(-vt, e, v);     // v - hv
+  return v >= 0.f ? pos : hv;
+}
+
+MICLIP_DEV f32x2 gelu_erf2(f32x2 v) {
+  using namespace gelu_nr;
+  const f32x2 a = {__builtin_fabsf(v[0]), __builtin_fabsf(v[1])};
+  const f32x2 d = __builtin_elementwise_fma(a, (f32x2){kT, kT}, (f32x2){1.0f, 1.0f});
+  const f32x2 t = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+  f32x2 p = {kC[0], kC[0]};
+#pragma unroll
+  for (int i = 1; i < 10; ++i) p = __builtin_elementwise_fma(t, p, (f32x2){kC[i], kC[i]});
+  const f32x2 vt = v * t;
+  const f32x2 x = __builtin_elementwise_fma(v * v, (f32x2){kQ, kQ}, p);
+  const f32x2 e = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+  const f32x2 hv = vt * e;
+  const f32x2 pos = __builtin_elementwise_fma(-vt, e, v);
+  return (f32x2){v[0] >= 0.f ? pos[0] : hv[0], v[1] >= 0.f ? pos[1] : hv[1]};
+}
+
+template <int ACT>
+MICLIP_DEV float act_fn(float v) {
+  // x * sigmoid(1.702 x) (clip/model.py:160-162): v_exp + v_rcp, no IEEE divide
+  if (ACT == ACT_QUICKGELU) return v * __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v));
+  if (ACT == ACT_GELU) return gelu_erf(v);
+  return v;
+}
+
+// The activation is a template parameter so that the QKV projection (no
+// activation) and the MLP c_fc (QuickGELU) are distinct kernels in a profile.
+template <typename T, int ACT>
+struct EpiStore {
+  T* C;
+  const float* bias;
+  int ldc;
+  MICLIP_DEV float4 bias4(int col) const { return ld_bias4(bias, col); }
+  MICLIP_DEV float4 bias4nb(int col) const { return ld_bias4_nb(bias, col); }
+  MICLIP_DEV float bias1(int col) const { return bias ? bias[col] : 0.f; }
+  // The fp32 result is pinned in a register before the conversion: otherwise
+  // hipcc may fuse the last multiply (or add) with the conversion into one
+  // v_fma_mix* (a single rounding) in some call sites and not in others, and
+  // the tile and tail paths would differ in the last bit.
+  MICLIP_DEV static float fin(float y) {
+    asm volatile("" : "+v"(y));
+    return y;
+  }
+  template <bool ASM = false>
+  MICLIP_DEV void put4(int r, int c, float4 v, float4 b) const {
+    i16x4 o;
+    if constexpr (ACT == ACT_GELU) {  // packed-fp32 form (v_pk_fma_f32), same rounding
+      const f32x2 lo = gelu_erf2((f32x2){v.x + b.x, v.y + b.y});
+      const f32x2 hi = gelu_erf2((f32x2){v.z + b.z, v.w + b.w});
+      o[0] = to_bits<T>(fin(lo[0]));
+      o[1] = to_bits<T>(fin(lo[1]));
+      o[2] = to_bits<T>(fin(hi[0]));
+      o[3] = to_bits<T>(fin(hi[1]));
+    } else {
+      o[0] = to_bits<T>(fin(act_fn<ACT>(v.x + b.x)));
+      o[1] = to_bits<T>(fin(act_fn<ACT>(v.y + b.y)));
+      o[2] = to_bits<T>(fin(act_fn<ACT>(v.z + b.z)));
+      o[3] = to_bits<T>(fin(act_fn<ACT>(v.w + b.w)));
+    }
+    if constexpr (ASM)
+      st_b64_asm(C + (size_t)r * ldc + c, o);
+    else
+      *(i16x4*)(C + (size_t)r * ldc + c) = o;
+  }
+  MICLIP_DEV void put1(int r, int c, float v, float b) const {
+    C[(size_t)r * ldc + c] = to_t<T>(fin(act_fn<ACT>(v + b)));
+  }
+};
+
+// Residual stream X (R = float, or _Float16 as in the reference's fp16 GPU
+// model, clip/model.py:184-185 `x = x + ...` on half tensors) += acc + bias.
+// fp16: one rounding of x + (acc + bias) (the reference rounds acc + bias
+// first), pinned by fin so the tile and tail paths round alike.
+template <typename R>
+struct EpiResidual {
+  R* X;
+  const float* bias;
+  int ldx;
+  MICLIP_DEV float4 bias4(int col) const { return ld_bias4(bias, col); }
+  MICLIP_DEV float4 bias4nb(int col) const { return ld_bias4_nb(bias, col); }
+  MICLIP_DEV float bias1(int col) const { return bias[col]; }
+  MICLIP_DEV static float fin(float y) {
+    asm volatile("" : "+v"(y));
+    return y;
+  }
+  template <bool ASM = false>
+  MICLIP_DEV void put4(int r, int c, float4 v, float4 b) const {
+    if constexpr (std::is_same_v<R, float>) {
+      float4* p = (float4*)(X + (size_t)r * ldx + c);
+      const float4 x = *p;
+      const float4 y = make_float4(x.x + (v.x + b.x), x.y + (v.y + b.y), x.z + (v.z + b.z),
+                                   x.w + (v.w + b.w));
+      if constexpr (ASM)
+        st_b128_asm(p, y);
+      else
+        *p = y;
+    } else {
+      i16x4* p = (i16x4*)(X + (size_t)r * ldx + c);
+      const i16x4 x = *p;
+      i16x4 o;
+      o[0] = to_bits<R>(fin(from_bits<R>(x[0]) + (v.x + b.x)));
+      o[1] = to_bits<R>(fin(from_bits<R>(x[1]) + (v.y + b.y)));
+      o[2] = to_bits<R>(fin(from_bits<R>(x[2]) + (v.z + b.z)));
+      o[3] = to_bits<R>(fin(from_bits<R>(x[3]) + (v.w + b.w)));
+      if constexpr (ASM)
+        st_b64_asm(p, o);
+      else
+        *p = o;
+    }
+  }
+  MICLIP_DEV void put1(int r, int c, float v, float b) const {
+    R* p = X + (size_t)r * ldx + c;
+    if constexpr (std::is_same_v<R, float>)
+      *p = *p + (v + b);
+    else
+      *p = to_t<R>(fin((float)*p + (v + b)));
+  }
+};
+
+struct EpiF32 {
+  float* C;
+  const float* bias;
+  int ldc;
+  MICLIP_DEV float4 bias4(int col) const { return ld_bias4(bias, col); }
+  MICLIP_DEV float4 bias4nb(int col) const { return ld_bias4_nb(bias, col); }
+  MICLIP_DEV float bias1(int col) const { return bias ? bias[col] : 0.f; }
+  template <bool ASM = false>
+  MICLIP_DEV void put4(int r, int c, float4 v, float4 b) const {
+    const float4 y = make_float4(v.x + b.x, v.y + b.y, v.z + b.z, v.w + b.w);
+    if constexpr (ASM)
+      st_b128_asm(C + (size_t)r * ldc + c, y);
+    else
+      *(float4*)(C + (size_t)r * ldc + c) = y;
+  }
+  MICLIP_DEV void put1(int r, int c, float v, float b) const { C[(size_t)r * ldc + c] = v + b; }
+};
+
+// Diagnostic: stores only when the (impossible) flag is set, so the MFMA work
+// stays live but no output traffic is generated. Used to price the epilogue.
+struct EpiNull {
+  float* C;
+  int flag;
+  MICLIP_DEV float4 bias4(int) const { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  MICLIP_DEV float4 bias4nb(int) const { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  MICLIP_DEV float bias1(int) const { return 0.f; }
+  template <bool ASM = false>
+  MICLIP_DEV void put4(int r, int c, float4 v, float4) const {
+    if (flag == 12345) *(float4*)(C + c) = v;
+  }
+  MICLIP_DEV void put1(int r, int c, float v, float) const {
+    if (flag == 12345) C[c] = v;
+  }
+};
+
+template <typename R>
+struct EpiPatch {
+  R* X;
+  const float* pos;
+  int ldx;
+  int np;
+  MICLIP_DEV float4 bias4(int) const { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  MICLIP_DEV float4 bias4nb(int) const { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  MICLIP_DEV float bias1(int) const { return 0.f; }
+  MICLIP_DEV size_t row_of(int r) const {
+    const int b = r / np;
+    return (size_t)b * (np + 1) + 1 + (r - b * np);
+  }
+  template <bool ASM = false>
+  MICLIP_DEV void put4(int r, int c, float4 v, float4) const {
+    const int p = r % np;
+    const float4 q = *(const float4*)(pos + (size_t)(1 + p) * ldx + c);
+    const float4 y = make_float4(v.x + q.x, v.y + q.y, v.z + q.z, v.w + q.w);
+    if constexpr (std::is_same_v<R, float>) {
+      if constexpr (ASM)
+        st_b128_asm(X + row_of(r) * ldx + c, y);
+      else
+        *(float4*)(X + row_of(r) * ldx + c) = y;
+    } else {
+      i16x4 o;
+      o[0] = to_bits<R>(EpiResidual<R>::fin(y.x));
+      o[1] = to_bits<R>(EpiResidual<R>::fin(y.y));
+      o[2] = to_bits<R>(EpiResidual<R>::fin(y.z));
+      o[3] = to_bits<R>(EpiResidual<R>::fin(y.w));
+      *(i16x4*)(X + row_of(r) * ldx + c) = o;
+    }
+  }
+  MICLIP_DEV void put1(int r, int c, float v, float) const {
+    X[row_of(r) * ldx + c] =
+        to_t<R>(EpiResidual<R>::fin(v + pos[(size_t)(1 + r % np) * ldx + c]));
+  }
+};
+
+}  // namespace
+
+}  // namespace miclip

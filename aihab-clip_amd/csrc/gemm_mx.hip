@@ -1,0 +1,399 @@
+// MX-fp8 GEMM (stretch config C5: fp8 weights for the
+// open_clip ViT-H/14 shapes) on gfx950's block-scaled matrix cores.
+//
+// Operands are OCP MX-fp8: e4m3 elements with one E8M0 (power-of-two) scale per
+// 32 consecutive k of a row, i.e. per (row, k-block). The hardware applies the
+// scales inside v_mfma_scale_f32_16x16x128_f8f6f4, which runs at twice the
+// f16 rate (MI355X_MICROARCH.md, Matrix cores) -- no dequantisation anywhere.
+//
+// Lane maps (measured: scripts/probe/mx_probe.hip, mx_scale_probe.hip): lane l
+// holds row/col l&15; its 8 data VGPRs are the 16-B chunks g and 4+g
+// (g = l>>4) of the row's 128-byte K-tile -- the very chunks the f16 kernel's
+// two 16x16x32 k-steps read -- and its scale byte is that row's k-block g.
+// So one 128-k fp8 K-tile is byte-for-byte the f16 kernel's 64-k K-tile: the
+// same LDS-DMA staging, XOR swizzle and fragment reads, one MFMA where the
+// f16 kernel issues two, and half as many K-tiles.
+//
+// Scale planes are tiled for the kernel (mx_scale_index): per (256-row block,
+// 128-k tile) one 1-KiB block [k-block 4][row & 15][row >> 4 & 15], so a lane's
+// 8 A scales (rows wr*128 + qi*64 + i*16 + fr) are one ds_read_b64 and its 4 W
+// scales one ds_read_b32, selected per MFMA by the instruction's byte op_sel.
+// The scale blocks ride the A0 half-tile DMA (one global_load_lds_dword per
+// wave) into a 2 x 2 KiB LDS ring.
+//
+// Producers: `quant_mx` (weights at load, any fp32/fp16 rows), the LayerNorm
+// MX output (norm.hip) and the EpiMX epilogue below (c_fc + GELU -> MX for
+// c_proj). Quantisation rule: E = ceil(log2(amax / 448)) per block, elements
+// RNE to e4m3 (v_cvt_pk_fp8_f32) -- no element ever saturates.
+#include "common.h"
+#include "epilogue.h"
+#include "kernels.h"
+#include "mx.h"
+
+#include <cstdlib>
+
+namespace miclip {
+
+namespace {
+
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+// c_fc epilogue for the fp8 path: act(acc + bias) quantised to MX-fp8 rows of
+// the next GEMM's A operand (data [M, ldc] bytes + tiled scale plane). Called
+// by all 64 lanes of a wave with 4 consecutive columns each (the LDS-staged
+// epilogue: one row of 256 columns per wave instruction).
+template <int ACT>
+struct EpiMX {
+  uint8_t* C;
+  uint8_t* S;
+  const float* bias;
+  int ldc;
+  int kt;  // 128-k tiles per row of the output (= ldc / 128)
+  MICLIP_DEV float4 bias4(int col) const { return ld_bias4(bias, col); }
+  MICLIP_DEV float4 bias4nb(int col) const { return ld_bias4_nb(bias, col); }
+  MICLIP_DEV float bias1(int col) const { return bias ? bias[col] : 0.f; }
+  template <bool ASM = false>
+  MICLIP_DEV void put4(int r, int c, float4 v, float4 b) const {
+    float4 y;
+    if constexpr (ACT == ACT_GELU) {
+      const f32x2 lo = gelu_erf2((f32x2){v.x + b.x, v.y + b.y});
+      const f32x2 hi = gelu_erf2((f32x2){v.z + b.z, v.w + b.w});
+      y = make_float4(lo[0], lo[1], hi[0], hi[1]);
+    } else {
+      y = make_float4(act_fn<ACT>(v.x + b.x), act_fn<ACT>(v.y + b.y), act_fn<ACT>(v.z + b.z),
+                      act_fn<ACT>(v.w + b.w));
+    }
+    int e;
+    const unsigned q = mx_quant4(y, e);
+    *(unsigned*)(C + (size_t)r * ldc + c) = q;
+    if ((threadIdx.x & 7) == 0) S[mx_scale_index(r, c >> 5, kt)] = (uint8_t)(e + 127);
+  }
+};
+
+// 4-byte LDS-DMA of a scale block piece, issued from inline asm: with the
+// builtin, hipcc cannot tell the scale ring from the fragment slots and waits
+// vmcnt(0) before every scale ds_read (draining the K-tile pipeline). The
+// kernel's own counted waits cover it (3 ops per A0 stage). `lds` wave-uniform.
+MICLIP_DEV void glds4_hidden(const void* g, const void* lds) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(const LDS_AS void*)lds);
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g), "s"(dst)
+      : "memory");
+}
+
+// The scaled MFMAs have no memory side effects, and without a scheduling
+// fence hipcc sinks all of a K-tile's MFMAs below the phase barriers (every
+// phase's fragments then stay live: 256 VGPRs and spills). sched_barrier(0)
+// keeps each phase's MFMAs between its barriers, as in gemm256_kernel.
+MICLIP_DEV void lds_barrier_mx() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// 256x256x128(fp8) tile, 8 waves 2(M) x 4(N), the staggered 8-phase schedule of
+// gemm256_kernel<SCHED 2> (gemm.hip; cdna_hip_programming.md §5 "256^2 8-phase
+// template"). vmcnt counts include the scale DMA (3 ops in every A0 stage).
+template <class Epi>
+__global__ __launch_bounds__(512) void gemm256_mx_kernel(const uint8_t* __restrict__ A,
+                                                         const uint8_t* __restrict__ SA,
+                                                         const uint8_t* __restrict__ W,
+                                                         const uint8_t* __restrict__ SW, int M,
+                                                         int N, int K, Epi epi, int gm) {
+  constexpr int HALF = 128 * 128;      // bytes of one half-tile slot
+  constexpr int EPI_LD = 260;          // fp32 row stride of the epilogue staging
+  constexpr int SCL = 8 * HALF;        // scale ring: 2 x (A 1 KiB + W 1 KiB)
+  constexpr int SMEM = 128 * EPI_LD * 4 > SCL + 4096 ? 128 * EPI_LD * 4 : SCL + 4096;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const int ntn = N / 256, ntm = (M + 255) / 256, ndp = ntm * ntn;
+  const int KT = K / 128, nk = KT;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  int tm, tn;
+  group_tile(xcd_remap(blockIdx.x, ndp), ntm, ntn, gm, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int lchunk = (lane & 7) ^ (lane >> 3);
+  const uint8_t* asrc[2][2];
+  const uint8_t* bsrc[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      const int sr = (wave * 2 + pp) * 8 + (lane >> 3);
+      int ar = m0 + (sr >> 6) * 128 + h * 64 + (sr & 63);
+      ar = ar < M ? ar : M - 1;
+      asrc[h][pp] = A + (size_t)ar * K + lchunk * 16;
+      const int bc = n0 + (sr >> 5) * 64 + h * 32 + (sr & 31);
+      bsrc[h][pp] = W + (size_t)bc * K + lchunk * 16;
+    }
+  // scale DMA source of this wave: waves 0-3 the A block, 4-7 the W block
+  const uint8_t* ssrc = (wave < 4 ? SA + (size_t)tm * KT * 1024 : SW + (size_t)tn * KT * 1024) +
+                        (wave & 3) * 256 + lane * 4;
+  auto stage = [&](int slot_kind, int tile) {
+    const int buf = tile & 1, k0 = tile * 128;
+    char* dst = smem + (buf * 4 + slot_kind) * HALF + wave * 2048;
+    const uint8_t* const* src = slot_kind < 2 ? asrc[slot_kind] : bsrc[slot_kind - 2];
+    glds16(src[0] + k0, dst);
+    glds16(src[1] + k0, dst + 1024);
+    if (slot_kind == 0)
+      glds4_hidden(ssrc + (size_t)tile * 1024,
+                   smem + SCL + buf * 2048 + (wave >> 2) * 1024 + (wave & 3) * 256);
+  };
+  const int fr = lane & 15, fk = lane >> 4;
+  const int aoff = (wr * 64 + fr) * 128, boff = (wc * 32 + fr) * 128;
+  const int sw0 = ((0 + fk) ^ (fr & 7)) << 4, sw1 = ((4 + fk) ^ (fr & 7)) << 4;
+  const int soa = fk * 256 + fr * 16 + wr * 8, sob = 1024 + fk * 256 + fr * 16 + wc * 4;
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // 8-VGPR fragments: two ds_read_b128 joined into a freshly defined v8i (a
+  // partial .lo/.hi update keeps the old tuple live and doubles the registers)
+  v8i af[4], bf[2];
+  unsigned sa[2], sb = 0;
+  auto rd8 = [&](const char* p0, const char* p1) {
+    const i32x4 lo = *(const i32x4*)p0, hi = *(const i32x4*)p1;
+    return (v8i)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  auto quadrant = [&](const char* sa_, const char* sb_, bool load_a) {
+    if (load_a) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = rd8(sa_ + i * 2048 + sw0, sa_ + i * 2048 + sw1);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bf[j] = rd8(sb_ + j * 2048 + sw0, sb_ + j * 2048 + sw1);
+  };
+  auto mfma_q = [&](int qi, int qj) {
+    // op_sel picks the scale byte: A slot qi*4 + i -> dword qi, byte i; W slot
+    // qj*2 + j -> byte qj*2 + j, i.e. byte j of sb >> 16*qj. The op_sel values
+    // must be immediates, so they depend on the unrolled i / j only.
+    const int sca = qi ? (int)sa[1] : (int)sa[0];
+    const int scb = qj ? (int)(sb >> 16) : (int)sb;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+#define MICLIP_MXM(IA, IB)                                                                   \
+  acc[qi][qj][i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bf[j],        \
+                                                                       acc[qi][qj][i][j], 0, \
+                                                                       0, IA, sca, IB, scb)
+        if (j == 0) {
+          if (i == 0) MICLIP_MXM(0, 0); else if (i == 1) MICLIP_MXM(1, 0);
+          else if (i == 2) MICLIP_MXM(2, 0); else MICLIP_MXM(3, 0);
+        } else {
+          if (i == 0) MICLIP_MXM(0, 1); else if (i == 1) MICLIP_MXM(1, 1);
+          else if (i == 2) MICLIP_MXM(2, 1); else MICLIP_MXM(3, 1);
+        }
+#undef MICLIP_MXM
+      }
+    // pin this phase's MFMAs before the next barrier (see lds_barrier_mx)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(acc[qi][qj][i][j]));
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: A0(0)+S(0) B1(0) A1(0) B0(0) A0(1)+S(1) B1(1)
+  stage(0, 0);
+  stage(3, 0);
+  stage(1, 0);
+  stage(2, 0);
+  if (nk > 1) {
+    stage(0, 1);
+    stage(3, 1);
+    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  lds_barrier_mx();
+  if (wr == 1) lds_barrier_mx();   // stagger (wave-uniform)
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    const char* sA0 = smem + (buf * 4 + 0) * HALF + aoff;
+    const char* sA1 = smem + (buf * 4 + 1) * HALF + aoff;
+    const char* sB0 = smem + (buf * 4 + 2) * HALF + boff;
+    const char* sB1 = smem + (buf * 4 + 3) * HALF + boff;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      if (p == 0 && wr == 0 && t > 0) {
+        if (t + 1 < nk)
+          asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      if (p == 3 && wr == 1 && t + 1 < nk) {
+        if (t + 2 < nk)
+          asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      const int qi = (p >= 2) ? 1 : 0;
+      const int qj = (p == 1 || p == 2) ? 1 : 0;
+      quadrant(qi ? sA1 : sA0, qj ? sB1 : sB0, p == 0 || p == 2);
+      if (p == 0) {
+        // this K-tile's scales (they arrived with A0(t)). Read from inline asm
+        // that also retires them (lgkmcnt(0), which the phase waits for anyway):
+        // a plain ds_read here gets a compiler vmcnt(0) in front of it, since
+        // hipcc cannot prove the ring disjoint from the in-flight slot DMA.
+        const unsigned base = (unsigned)(size_t)(const LDS_AS void*)(smem + SCL + buf * 2048);
+        u32x2 s2;
+        asm volatile(
+            "ds_read_b64 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+            : "=v"(s2), "=v"(sb)
+            : "v"(base + soa), "v"(base + sob)
+            : "memory");
+        sa[0] = s2[0];
+        sa[1] = s2[1];
+      }
+      if (p == 0 && t + 1 < nk) stage(1, t + 1);
+      if (p == 1 && t + 1 < nk) stage(2, t + 1);
+      if (p == 2 && t + 2 < nk) stage(0, t + 2);
+      if (p == 3 && t + 2 < nk) stage(3, t + 2);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      lds_barrier_mx();
+      mfma_q(qi, qj);
+      lds_barrier_mx();
+    }
+  }
+  if (wr == 0) lds_barrier_mx();   // balance the stagger barrier
+
+  // LDS-staged epilogue (as gemm256_kernel): 2 passes of 128 fp32 rows
+  float* stg = (float*)smem;
+  const int ec = (tid & 63) * 4;
+  const float4 bv = epi.bias4(n0 + ec);
+  const bool full = m0 + 256 <= M;
+#pragma unroll
+  for (int qi = 0; qi < 2; ++qi) {
+    lds_barrier_mx();
+#pragma unroll
+    for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int lr = wr * 64 + i * 16 + fk * 4 + r;
+            const int lc = wc * 64 + qj * 32 + j * 16 + fr;
+            stg[lr * EPI_LD + lc] = acc[qi][qj][i][j][r];
+          }
+    lds_barrier_mx();
+    if (full) {
+#pragma unroll 4
+      for (int k = 0; k < 16; ++k) {
+        const int lr = (tid >> 6) + 8 * k;
+        const int row = m0 + (lr >> 6) * 128 + qi * 64 + (lr & 63);
+        epi.put4(row, n0 + ec, *(const float4*)(stg + lr * EPI_LD + ec), bv);
+      }
+    } else {
+#pragma unroll 4
+      for (int k = 0; k < 16; ++k) {
+        const int lr = (tid >> 6) + 8 * k;
+        const int row = m0 + (lr >> 6) * 128 + qi * 64 + (lr & 63);
+        if (row < M) epi.put4(row, n0 + ec, *(const float4*)(stg + lr * EPI_LD + ec), bv);
+      }
+    }
+  }
+}
+
+// Rows of fp32 / fp16 -> MX-fp8 (data + tiled scales). One wave per 256
+// consecutive k of one row (8 blocks of 32, 4 elements per lane).
+template <typename TI>
+__global__ __launch_bounds__(256) void quant_mx_kernel(const TI* __restrict__ in, int R, int K,
+                                                       uint8_t* __restrict__ q,
+                                                       uint8_t* __restrict__ sc) {
+  const int lane = threadIdx.x & 63;
+  const int seg = blockIdx.x * 4 + (threadIdx.x >> 6);   // (row, 256-k segment)
+  const int nseg = K / 256;
+  const int r = seg / nseg, k = (seg - r * nseg) * 256 + 4 * lane;
+  if (r >= R) return;
+  float4 v;
+  if constexpr (std::is_same_v<TI, float>) {
+    v = *(const float4*)(in + (size_t)r * K + k);
+  } else {
+    const i16x4 h = *(const i16x4*)(in + (size_t)r * K + k);
+    v = make_float4(from_bits<TI>(h[0]), from_bits<TI>(h[1]), from_bits<TI>(h[2]),
+                    from_bits<TI>(h[3]));
+  }
+  int e;
+  const unsigned w = mx_quant4(v, e);
+  *(unsigned*)(q + (size_t)r * K + k) = w;
+  if ((lane & 7) == 0) sc[mx_scale_index(r, k >> 5, K / 128)] = (uint8_t)(e + 127);
+}
+
+template <class Epi>
+hipError_t launch_mx(const void* A, const void* SA, const void* W, const void* SW, int M, int N,
+                     int K, Epi epi, hipStream_t s) {
+  if (M < 1 || N % 256 || K % 128 || K < 128) return hipErrorInvalidValue;
+  const int grid = (M + 255) / 256 * (N / 256);
+  const char* e = getenv("MICLIP_GEMM_GROUP");
+  const int gm = e ? (atoi(e) < 1 ? 1 : atoi(e)) : 4;
+  hipLaunchKernelGGL((gemm256_mx_kernel<Epi>), dim3(grid), dim3(512), 0, s, (const uint8_t*)A,
+                     (const uint8_t*)SA, (const uint8_t*)W, (const uint8_t*)SW, M, N, K, epi, gm);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+size_t mx_scale_bytes(int rows, int K) { return (size_t)((rows + 255) / 256) * (K / 128) * 1024; }
+
+hipError_t quant_mx(int in_f16, const void* in, int R, int K, void* q, void* sc, hipStream_t s) {
+  if (R < 1 || K % 256) return hipErrorInvalidValue;
+  const int segs = R * (K / 256);
+  if (in_f16)
+    hipLaunchKernelGGL(quant_mx_kernel<_Float16>, dim3((segs + 3) / 4), dim3(256), 0, s,
+                       (const _Float16*)in, R, K, (uint8_t*)q, (uint8_t*)sc);
+  else
+    hipLaunchKernelGGL(quant_mx_kernel<float>, dim3((segs + 3) / 4), dim3(256), 0, s,
+                       (const float*)in, R, K, (uint8_t*)q, (uint8_t*)sc);
+  return hipGetLastError();
+}
+
+hipError_t gemm_mx(const void* A, const void* SA, const void* W, const void* SW, const float* bias,
+                   void* C, void* CS, int M, int N, int K, int epi, int act, hipStream_t s) {
+  if (!A || !SA || !W || !SW || !C) return hipErrorInvalidValue;
+  switch (epi) {
+    case 0:   // fp16 store: act(acc + bias)
+      if (act == ACT_NONE)
+        return launch_mx(A, SA, W, SW, M, N, K, EpiStore<_Float16, ACT_NONE>{(_Float16*)C, bias, N}, s);
+      if (act == ACT_QUICKGELU)
+        return launch_mx(A, SA, W, SW, M, N, K,
+                         EpiStore<_Float16, ACT_QUICKGELU>{(_Float16*)C, bias, N}, s);
+      return launch_mx(A, SA, W, SW, M, N, K, EpiStore<_Float16, ACT_GELU>{(_Float16*)C, bias, N}, s);
+    case 1:   // fp16 residual stream += acc + bias
+      if (!bias) return hipErrorInvalidValue;
+      return launch_mx(A, SA, W, SW, M, N, K, EpiResidual<_Float16>{(_Float16*)C, bias, N}, s);
+    case 5:   // MX-fp8 out (data C [M, N] bytes + scale plane CS): act(acc + bias)
+      if (!CS || N % 128) return hipErrorInvalidValue;
+      if (act == ACT_QUICKGELU)
+        return launch_mx(A, SA, W, SW, M, N, K,
+                         EpiMX<ACT_QUICKGELU>{(uint8_t*)C, (uint8_t*)CS, bias, N, N / 128}, s);
+      if (act == ACT_GELU)
+        return launch_mx(A, SA, W, SW, M, N, K,
+                         EpiMX<ACT_GELU>{(uint8_t*)C, (uint8_t*)CS, bias, N, N / 128}, s);
+      return launch_mx(A, SA, W, SW, M, N, K,
+                       EpiMX<ACT_NONE>{(uint8_t*)C, (uint8_t*)CS, bias, N, N / 128}, s);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace miclip

@@ -33,15 +33,29 @@ hipError_t gemm_null(int dtype, const void* A, const void* W, float* C, int M, i
 hipError_t gemm_patch(int dtype, const void* A, const void* W, const float* pos, void* X,
                       int M, int N, int K, int np, hipStream_t s, int resid16 = 0);
 
+// ---- MX-fp8 (OCP e4m3 + E8M0 per 32 k) operands and GEMM (gemm_mx.hip) ----
+// Scale plane bytes of a [rows, K] operand (tiled, see mx_scale_index).
+size_t mx_scale_bytes(int rows, int K);
+// Rows [R, K] (fp32, or fp16 when in_f16; K % 256 == 0) -> data q [R, K] bytes + scales sc.
+hipError_t quant_mx(int in_f16, const void* in, int R, int K, void* q, void* sc, hipStream_t s);
+// C = A[M,K] . W[N,K]^T with MX-fp8 operands (N % 256 == 0, K % 128 == 0).
+// epi 0: C fp16 = act(acc + bias); epi 1: C fp16 residual += acc + bias;
+// epi 5: C MX-fp8 data [M, N] + scale plane CS = MX(act(acc + bias)).
+hipError_t gemm_mx(const void* A, const void* SA, const void* W, const void* SW, const float* bias,
+                   void* C, void* CS, int M, int N, int K, int epi, int act, hipStream_t s);
+
 // ---- LayerNorm (fp32 statistics, eps 1e-5) over rows of width D ----
 // Row r of the input is at in + in_row(r)*D with in_row(r) = rows ? rows[r] : r*in_stride_rows;
 // the input is fp32, or fp16 when in16 (fp16 residual stream).
 // out_f32 != null -> fp32 output (may alias an fp32 in); else out_t in compute dtype (may
 // alias an fp16 in of the same dtype).
 // normalize != 0 additionally L2-normalises each output row (F.normalize, eps 1e-12).
+// out_q != null: MX-fp8 output instead (data out_q [R, D] bytes + tiled scale plane
+// out_s, the fp8 GEMM's A operand).
 hipError_t layernorm(int dtype, const void* in, const int32_t* rows, int in_stride_rows,
                      const float* gamma, const float* beta, float* out_f32, void* out_t,
-                     int R, int D, int normalize, hipStream_t s, int in16 = 0);
+                     int R, int D, int normalize, hipStream_t s, int in16 = 0,
+                     void* out_q = nullptr, void* out_s = nullptr);
 
 // ---- fused multi-head attention over a packed QKV buffer ----
 // qkv: [B*N, 3*H*dh] compute dtype (torch in_proj order q|k|v); out: [B*N, H*dh].

@@ -10,6 +10,7 @@
 // gathered rows are never materialised.
 #include "common.h"
 #include "kernels.h"
+#include "mx.h"
 
 namespace miclip {
 
@@ -35,7 +36,8 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* in,  // may al
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta,
                                                         float* out_f32, T* out_t, int R, int D,
-                                                        int normalize) {
+                                                        int normalize, uint8_t* out_q,
+                                                        uint8_t* out_s) {
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= R) return;
@@ -75,7 +77,17 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* in,  // may al
       v[i].x *= inv; v[i].y *= inv; v[i].z *= inv; v[i].w *= inv;
     }
   }
-  if (out_f32) {
+  if (out_q) {
+    // MX-fp8 rows for the fp8 GEMM (gemm_mx.hip): 32-value block = 8 lanes
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      int e;
+      const unsigned q = mx_quant4(v[i], e);
+      const int k = i * 256 + 4 * lane;
+      *(unsigned*)(out_q + (size_t)r * D + k) = q;
+      if ((lane & 7) == 0) out_s[mx_scale_index(r, k >> 5, D / 128)] = (uint8_t)(e + 127);
+    }
+  } else if (out_f32) {
     float4* dst = (float4*)(out_f32 + (size_t)r * D);
 #pragma unroll
     for (int i = 0; i < VPL; ++i) dst[i * 64 + lane] = v[i];
@@ -95,12 +107,13 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* in,  // may al
 
 template <typename T, typename TI>
 hipError_t ln_dispatch(const TI* in, const int32_t* rows, int stride, const float* g,
-                       const float* b, float* of, void* ot, int R, int D, int nz, hipStream_t s) {
+                       const float* b, float* of, void* ot, int R, int D, int nz, hipStream_t s,
+                       uint8_t* oq, uint8_t* os) {
   const dim3 grid((R + 3) / 4), block(256);
 #define MICLIP_LN_CASE(V)                                                                       \
   case V:                                                                                       \
     hipLaunchKernelGGL((layernorm_kernel<V, T, TI>), grid, block, 0, s, in, rows, stride, g, b, \
-                       of, (T*)ot, R, D, nz);                                                   \
+                       of, (T*)ot, R, D, nz, oq, os);                                           \
     break;
   switch (D / 256) {
     MICLIP_LN_CASE(1)
@@ -120,18 +133,20 @@ hipError_t ln_dispatch(const TI* in, const int32_t* rows, int stride, const floa
 
 hipError_t layernorm(int dtype, const void* in, const int32_t* rows, int in_stride_rows,
                      const float* gamma, const float* beta, float* out_f32, void* out_t, int R,
-                     int D, int normalize, hipStream_t s, int in16) {
-  if (R < 1 || D % 256 || D > 1536 || (!out_f32 && !out_t)) return hipErrorInvalidValue;
+                     int D, int normalize, hipStream_t s, int in16, void* out_q, void* out_s) {
+  if (R < 1 || D % 256 || D > 1536 || (!out_f32 && !out_t && !out_q)) return hipErrorInvalidValue;
+  if (out_q && !out_s) return hipErrorInvalidValue;
+  uint8_t *oq = (uint8_t*)out_q, *os = (uint8_t*)out_s;
   if (in16) {  // fp16 residual stream: fp16 compute only
     if (dtype != kF16) return hipErrorInvalidValue;
     return ln_dispatch<_Float16>((const _Float16*)in, rows, in_stride_rows, gamma, beta, out_f32,
-                                 out_t, R, D, normalize, s);
+                                 out_t, R, D, normalize, s, oq, os);
   }
   if (dtype == kF16)
     return ln_dispatch<_Float16>((const float*)in, rows, in_stride_rows, gamma, beta, out_f32,
-                                 out_t, R, D, normalize, s);
+                                 out_t, R, D, normalize, s, oq, os);
   return ln_dispatch<__bf16>((const float*)in, rows, in_stride_rows, gamma, beta, out_f32, out_t,
-                             R, D, normalize, s);
+                             R, D, normalize, s, oq, os);
 }
 
 }  // namespace miclip

@@ -13,6 +13,7 @@ LIB_PATH = os.environ.get("MICLIP_LIB", os.path.join(_HERE, "libmiclip.so"))
 ABI_VERSION = 3          # include/miclip.h MICLIP_ABI_VERSION
 MICLIP_FP16 = 0
 MICLIP_BF16 = 1
+MICLIP_MXFP8 = 2
 MICLIP_ACT_QUICKGELU = 1
 MICLIP_ACT_GELU = 2
 MICLIP_FLAG_NORMALIZE = 1
@@ -25,6 +26,7 @@ EXPORTS = (
     "miclip_model_bytes", "miclip_set_profiling", "miclip_profile_read", "miclip_set_splits",
     "miclip_op_gemm", "miclip_op_layernorm", "miclip_op_attention", "miclip_preprocess",
     "miclip_row_norms", "miclip_class_centroids", "miclip_proto_scores",
+    "miclip_mx_scale_bytes", "miclip_op_quant_mx", "miclip_op_gemm_mx", "miclip_op_layernorm_mx",
 )
 
 MICLIP_PRE_F32 = 0
@@ -88,6 +90,11 @@ def load_library(path: str = None):
         "miclip_op_gemm": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp], ctypes.c_int),
         "miclip_op_layernorm": ([i32, vp, vp, vp, vp, i32, i32, i32, vp], ctypes.c_int),
         "miclip_op_attention": ([i32, vp, vp, i32, i32, i32, i32, i32, i32, vp], ctypes.c_int),
+        "miclip_mx_scale_bytes": ([i32, i32], i64),
+        "miclip_op_quant_mx": ([vp, i32, i32, i32, vp, vp, vp], ctypes.c_int),
+        "miclip_op_gemm_mx": ([vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
+                              ctypes.c_int),
+        "miclip_op_layernorm_mx": ([vp, i32, vp, vp, vp, vp, i32, i32, vp], ctypes.c_int),
         "miclip_preprocess": ([vp, vp, ctypes.POINTER(MiclipImageDesc), i32, vp, i32, vp],
                               ctypes.c_int),
         "miclip_row_norms": ([vp, i32, i32, vp, f32, vp, vp], ctypes.c_int),

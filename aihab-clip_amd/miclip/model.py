@@ -31,8 +31,10 @@ from torch import nn
 from . import _lib
 from .configs import CLIPConfig
 
+# "mxfp8": QKV / c_fc / c_proj on MX-fp8 operands, fp16 elsewhere
 _DTYPES = {"fp16": (_lib.MICLIP_FP16, torch.float16), "float16": (_lib.MICLIP_FP16, torch.float16),
-           "bf16": (_lib.MICLIP_BF16, torch.bfloat16), "bfloat16": (_lib.MICLIP_BF16, torch.bfloat16)}
+           "bf16": (_lib.MICLIP_BF16, torch.bfloat16), "bfloat16": (_lib.MICLIP_BF16, torch.bfloat16),
+           "mxfp8": (_lib.MICLIP_MXFP8, torch.float16)}
 
 
 class _Node(nn.Module):

@@ -37,7 +37,10 @@ enum miclip_status {
   MICLIP_ENOMEM = -4
 };
 
-enum miclip_dtype { MICLIP_FP16 = 0, MICLIP_BF16 = 1 };
+/* MICLIP_MXFP8: QKV, c_fc and c_proj on OCP MX-fp8 operands (e4m3 + an E8M0 scale
+ * per 32 k; weights quantised at load, activations by the producing kernels), the
+ * rest as MICLIP_FP16. SURVEY §8f row 4 (C5 fp8 weights); parity unpinned. */
+enum miclip_dtype { MICLIP_FP16 = 0, MICLIP_BF16 = 1, MICLIP_MXFP8 = 2 };
 enum miclip_act { MICLIP_ACT_QUICKGELU = 1, MICLIP_ACT_GELU = 2 };
 
 /* encode_image flags */
@@ -225,6 +228,22 @@ int miclip_op_layernorm(int32_t dtype, const void* in, const float* gamma, const
 int miclip_op_attention(int32_t dtype, const void* qkv, void* out, int32_t B, int32_t N,
                         int32_t H, int32_t head_dim, int32_t causal, int32_t variant,
                         void* stream);
+
+/* ---- MX-fp8 operands (MICLIP_MXFP8; no reference counterpart: C5 stretch) ----
+ * An MX-fp8 [rows, K] operand is e4m3 bytes [rows, K] plus a tiled E8M0 scale
+ * plane of miclip_mx_scale_bytes(rows, K) bytes (one scale per 32 consecutive k). */
+int64_t miclip_mx_scale_bytes(int32_t rows, int32_t K);
+/* rows [R, K] (fp32, or fp16 if in_f16; K % 256 == 0) -> q [R, K] + scales */
+int miclip_op_quant_mx(const void* in, int32_t in_f16, int32_t R, int32_t K, void* q, void* scales,
+                       void* stream);
+/* C = A . W^T on MX-fp8 operands (N % 256 == 0, K % 128 == 0). epi 0: C fp16 =
+ * act(. + bias); epi 1: C fp16 += . + bias; epi 5: C MX-fp8 (+ CS scales) = MX(act(. + bias)). */
+int miclip_op_gemm_mx(const void* A, const void* SA, const void* W, const void* SW,
+                      const float* bias, void* C, void* CS, int32_t M, int32_t N, int32_t K,
+                      int32_t epi, int32_t act, void* stream);
+/* LayerNorm (fp32 in, or fp16 if in_f16) -> MX-fp8 rows q [R, D] + scales */
+int miclip_op_layernorm_mx(const void* in, int32_t in_f16, const float* gamma, const float* beta,
+                           void* q, void* scales, int32_t R, int32_t D, void* stream);
 
 #ifdef __cplusplus
 }

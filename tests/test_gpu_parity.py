@@ -203,3 +203,24 @@ def test_zero_shot_head_vs_torch(B, C, k):
     nf = torch.nn.functional.normalize(feats @ m.visual.proj, dim=-1)
     l2, _ = m.zero_shot(nf, tw, 100.0, k=0, apply_proj=False)
     assert (l2 - ref).abs().max().item() < 2e-3
+
+
+# MICLIP_MXFP8: parity unpinned with respect to the
+# reference (no fp8 path there); bounded against the fp32 goldens with an fp8
+# tolerance instead of COS_TOL.
+MX_COS_TOL = 2e-2
+
+
+@pytest.mark.parametrize("tag,name", [("vitb32", "ViT-B/32"), ("vith14", "ViT-H-14")])
+def test_mxfp8_encode_within_fp8_tolerance(golden, tag, name):
+    from miclip.configs import MODEL_CONFIGS
+    from miclip.weights import synthetic_images
+    g = golden(tag)
+    imgs = synthetic_images(g["meta"]["n_images"], MODEL_CONFIGS[name].image_resolution, seed=0)
+    m = _model(name, "mxfp8")
+    feats = m.encode_image(torch.from_numpy(imgs).cuda()).cpu()
+    d = _one_minus_cos(feats, g["image"])
+    xb, xp = m.encode_text(torch.from_numpy(g["tokens"]).long().cuda())
+    dt = _one_minus_cos(xp.cpu(), g["text_proj"])
+    print(f"{tag}/mxfp8: image 1-cos max {d.max():.2e}, text 1-cos max {dt.max():.2e}")
+    assert d.max() <= MX_COS_TOL and dt.max() <= MX_COS_TOL
