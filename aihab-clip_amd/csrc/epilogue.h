@@ -90,10 +90,24 @@ MICLIP_DEV f32x2 gelu_erf2(f32x2 v) {
   return (f32x2){v[0] >= 0.f ? pos[0] : hv[0], v[1] >= 0.f ? pos[1] : hv[1]};
 }
 
+constexpr float kQuickGeluK = -1.702f * 1.4426950408889634f;
+
+// QuickGELU on two values with packed fp32 mul / add (v_pk_mul_f32, v_pk_add_f32):
+// the c_fc epilogue is VALU-bound, and these round exactly like the scalar form.
+MICLIP_DEV f32x2 quick_gelu2(f32x2 v) {
+  const f32x2 t = v * (f32x2){kQuickGeluK, kQuickGeluK};
+  const f32x2 d = (f32x2){__builtin_amdgcn_exp2f(t[0]), __builtin_amdgcn_exp2f(t[1])} +
+                  (f32x2){1.0f, 1.0f};
+  return v * (f32x2){__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+}
+
 template <int ACT>
 MICLIP_DEV float act_fn(float v) {
-  // x * sigmoid(1.702 x) (clip/model.py:160-162): v_exp + v_rcp, no IEEE divide
-  if (ACT == ACT_QUICKGELU) return v * __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v));
+  // x * sigmoid(1.702 x) (clip/model.py:160-162): one mul into v_exp (base 2,
+  // -1.702 log2 e folded), v_rcp, no IEEE divide; same op sequence as the
+  // packed quick_gelu2 below
+  if (ACT == ACT_QUICKGELU)
+    return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(v * kQuickGeluK));
   if (ACT == ACT_GELU) return gelu_erf(v);
   return v;
 }
@@ -119,9 +133,11 @@ struct EpiStore {
   template <bool ASM = false>
   MICLIP_DEV void put4(int r, int c, float4 v, float4 b) const {
     i16x4 o;
-    if constexpr (ACT == ACT_GELU) {  // packed-fp32 form (v_pk_fma_f32), same rounding
-      const f32x2 lo = gelu_erf2((f32x2){v.x + b.x, v.y + b.y});
-      const f32x2 hi = gelu_erf2((f32x2){v.z + b.z, v.w + b.w});
+    if constexpr (ACT == ACT_GELU || ACT == ACT_QUICKGELU) {  // packed-fp32 forms, same rounding
+      const f32x2 y0 = (f32x2){v.x, v.y} + (f32x2){b.x, b.y};
+      const f32x2 y1 = (f32x2){v.z, v.w} + (f32x2){b.z, b.w};
+      const f32x2 lo = ACT == ACT_GELU ? gelu_erf2(y0) : quick_gelu2(y0);
+      const f32x2 hi = ACT == ACT_GELU ? gelu_erf2(y1) : quick_gelu2(y1);
       o[0] = to_bits<T>(fin(lo[0]));
       o[1] = to_bits<T>(fin(lo[1]));
       o[2] = to_bits<T>(fin(hi[0]));
