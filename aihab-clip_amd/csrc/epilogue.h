@@ -186,18 +186,25 @@ struct EpiResidual {
       else
         *p = y;
     } else {
-      i16x4* p = (i16x4*)(X + (size_t)r * ldx + c);
-      const i16x4 x = *p;
-      i16x4 o;
-      o[0] = to_bits<R>(fin(from_bits<R>(x[0]) + (v.x + b.x)));
-      o[1] = to_bits<R>(fin(from_bits<R>(x[1]) + (v.y + b.y)));
-      o[2] = to_bits<R>(fin(from_bits<R>(x[2]) + (v.z + b.z)));
-      o[3] = to_bits<R>(fin(from_bits<R>(x[3]) + (v.w + b.w)));
-      if constexpr (ASM)
-        st_b64_asm(p, o);
-      else
-        *p = o;
+      put4x<ASM>(r, c, v, b, load4(r, c));
     }
+  }
+  // fp16 stream, split form for the LDS-staged epilogues: a pass's 16 residual
+  // rows are loaded (load4) before the accumulators are staged, so their latency
+  // hides under the LDS writes instead of sitting in front of every store.
+  MICLIP_DEV i16x4 load4(int r, int c) const { return *(const i16x4*)(X + (size_t)r * ldx + c); }
+  template <bool ASM = false>
+  MICLIP_DEV void put4x(int r, int c, float4 v, float4 b, i16x4 x) const {
+    i16x4 o;
+    o[0] = to_bits<R>(fin(from_bits<R>(x[0]) + (v.x + b.x)));
+    o[1] = to_bits<R>(fin(from_bits<R>(x[1]) + (v.y + b.y)));
+    o[2] = to_bits<R>(fin(from_bits<R>(x[2]) + (v.z + b.z)));
+    o[3] = to_bits<R>(fin(from_bits<R>(x[3]) + (v.w + b.w)));
+    i16x4* p = (i16x4*)(X + (size_t)r * ldx + c);
+    if constexpr (ASM)
+      st_b64_asm(p, o);
+    else
+      *p = o;
   }
   MICLIP_DEV void put1(int r, int c, float v, float b) const {
     R* p = X + (size_t)r * ldx + c;
@@ -207,6 +214,11 @@ struct EpiResidual {
       *p = to_t<R>(fin((float)*p + (v + b)));
   }
 };
+
+// Epilogues whose put4 reads the output first (fp16 residual stream): the
+// staged epilogues prefetch those reads (load4 / put4x).
+template <class Epi> struct PrefetchX : std::false_type {};
+template <> struct PrefetchX<EpiResidual<_Float16>> : std::true_type {};
 
 struct EpiF32 {
   float* C;

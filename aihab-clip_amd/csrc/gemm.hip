@@ -703,6 +703,15 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
 #pragma unroll
   for (int qi = 0; qi < 2; ++qi) {
     lds_barrier();
+    i16x4 xr[16];
+    if constexpr (PrefetchX<Epi>::value) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int lr = (tid >> 6) + 8 * k;
+        const int row = m0 + (lr >> 6) * 128 + qi * 64 + (lr & 63);
+        xr[k] = epi.load4(row < M ? row : M - 1, n0 + ec);
+      }
+    }
 #pragma unroll
     for (int qj = 0; qj < 2; ++qj)
 #pragma unroll
@@ -716,7 +725,15 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
             stg[lr * EPI_LD + lc] = acc[qi][qj][i][j][r];
           }
     lds_barrier();
-    if (full) {
+    if constexpr (PrefetchX<Epi>::value) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int lr = (tid >> 6) + 8 * k;
+        const int row = m0 + (lr >> 6) * 128 + qi * 64 + (lr & 63);
+        if (full || row < M)
+          epi.put4x(row, n0 + ec, *(const float4*)(stg + lr * EPI_LD + ec), bv, xr[k]);
+      }
+    } else if (full) {
 #pragma unroll 4
       for (int k = 0; k < 16; ++k) {
         const int lr = (tid >> 6) + 8 * k;                      // 0..127

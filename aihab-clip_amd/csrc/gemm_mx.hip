@@ -283,6 +283,15 @@ __global__ __launch_bounds__(512) void gemm256_mx_kernel(const uint8_t* __restri
 #pragma unroll
   for (int qi = 0; qi < 2; ++qi) {
     lds_barrier_mx();
+    i16x4 xr[16];
+    if constexpr (PrefetchX<Epi>::value) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int lr = (tid >> 6) + 8 * k;
+        const int row = m0 + (lr >> 6) * 128 + qi * 64 + (lr & 63);
+        xr[k] = epi.load4(row < M ? row : M - 1, n0 + ec);
+      }
+    }
 #pragma unroll
     for (int qj = 0; qj < 2; ++qj)
 #pragma unroll
@@ -296,7 +305,15 @@ __global__ __launch_bounds__(512) void gemm256_mx_kernel(const uint8_t* __restri
             stg[lr * EPI_LD + lc] = acc[qi][qj][i][j][r];
           }
     lds_barrier_mx();
-    if (full) {
+    if constexpr (PrefetchX<Epi>::value) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int lr = (tid >> 6) + 8 * k;
+        const int row = m0 + (lr >> 6) * 128 + qi * 64 + (lr & 63);
+        if (full || row < M)
+          epi.put4x(row, n0 + ec, *(const float4*)(stg + lr * EPI_LD + ec), bv, xr[k]);
+      }
+    } else if (full) {
 #pragma unroll 4
       for (int k = 0; k < 16; ++k) {
         const int lr = (tid >> 6) + 8 * k;
