@@ -105,6 +105,85 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* in,  // may al
   }
 }
 
+// fp16-in -> compute-dtype-out LayerNorm for the fp16 residual stream (the
+// per-block ln_1 / ln_2 and in-place ln_pre): two rows per wave, a half-wave
+// per row, 8 values per lane per 256 columns, so every load and store is 16 B
+// (the general kernel moves 8 B per lane for fp16). Sums over the 32 lanes of
+// a half-wave with DPP (quad_perm, row_half_mirror, row_mirror) and one
+// bpermute for the last step.
+MICLIP_DEV float half_sum(float x) {
+  x += dppf<0xB1>(x);    // quad_perm [1,0,3,2]
+  x += dppf<0x4E>(x);    // quad_perm [2,3,0,1]
+  x += dppf<0x141>(x);   // row_half_mirror (lane i <-> 7-i of its 8)
+  x += dppf<0x140>(x);   // row_mirror (lane i <-> 15-i of its 16)
+  return x + __shfl_xor(x, 16, 64);
+}
+
+template <int NI, typename T>
+__global__ __launch_bounds__(256) void layernorm_h2_kernel(const _Float16* in,  // may alias out
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           T* out, int R, int D) {
+  const int lane = threadIdx.x & 63, hl = lane & 31;
+  const int r = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  if ((blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 >= R) return;   // whole wave past the end
+  const bool valid = r < R;
+  const _Float16* src = in + (size_t)(valid ? r : R - 1) * D + hl * 8;
+  float v[NI][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const i16x8 h = *(const i16x8*)(src + i * 256);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[i][e] = from_bits<_Float16>(h[e]);
+    s += ((v[i][0] + v[i][1]) + (v[i][2] + v[i][3])) + ((v[i][4] + v[i][5]) + (v[i][6] + v[i][7]));
+  }
+  const float mean = half_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[i][e] -= mean;
+      q += v[i][e] * v[i][e];
+    }
+  const float rstd = rsqrtf(half_sum(q) / (float)D + 1e-5f);
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int c = i * 256 + hl * 8;
+    const float4 g0 = *(const float4*)(gamma + c), g1 = *(const float4*)(gamma + c + 4);
+    const float4 b0 = *(const float4*)(beta + c), b1 = *(const float4*)(beta + c + 4);
+    const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    i16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = to_bits<T>(v[i][e] * rstd * g[e] + b[e]);
+    if (valid) *(i16x8*)(out + (size_t)r * D + c) = o;
+  }
+}
+
+template <typename T>
+hipError_t ln_h2_dispatch(const _Float16* in, const float* g, const float* b, void* out, int R,
+                          int D, hipStream_t s) {
+  const dim3 grid((R + 7) / 8), block(256);
+#define MICLIP_LNH_CASE(V)                                                                       \
+  case V:                                                                                        \
+    hipLaunchKernelGGL((layernorm_h2_kernel<V, T>), grid, block, 0, s, in, g, b, (T*)out, R, D); \
+    break;
+  switch (D / 256) {
+    MICLIP_LNH_CASE(1)
+    MICLIP_LNH_CASE(2)
+    MICLIP_LNH_CASE(3)
+    MICLIP_LNH_CASE(4)
+    MICLIP_LNH_CASE(5)
+    MICLIP_LNH_CASE(6)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef MICLIP_LNH_CASE
+  return hipGetLastError();
+}
+
 template <typename T, typename TI>
 hipError_t ln_dispatch(const TI* in, const int32_t* rows, int stride, const float* g,
                        const float* b, float* of, void* ot, int R, int D, int nz, hipStream_t s,
@@ -139,6 +218,8 @@ hipError_t layernorm(int dtype, const void* in, const int32_t* rows, int in_stri
   uint8_t *oq = (uint8_t*)out_q, *os = (uint8_t*)out_s;
   if (in16) {  // fp16 residual stream: fp16 compute only
     if (dtype != kF16) return hipErrorInvalidValue;
+    if (out_t && !out_f32 && !out_q && !rows && in_stride_rows == 1 && !normalize)
+      return ln_h2_dispatch<_Float16>((const _Float16*)in, gamma, beta, out_t, R, D, s);
     return ln_dispatch<_Float16>((const _Float16*)in, rows, in_stride_rows, gamma, beta, out_f32,
                                  out_t, R, D, normalize, s, oq, os);
   }
