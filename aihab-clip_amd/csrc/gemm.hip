@@ -734,7 +734,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
           epi.put4x(row, n0 + ec, *(const float4*)(stg + lr * EPI_LD + ec), bv, xr[k]);
       }
     } else if (full) {
-#pragma unroll 4
+#pragma unroll
       for (int k = 0; k < 16; ++k) {
         const int lr = (tid >> 6) + 8 * k;                      // 0..127
         const int row = m0 + (lr >> 6) * 128 + qi * 64 + (lr & 63);

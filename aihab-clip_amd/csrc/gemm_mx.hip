@@ -314,7 +314,7 @@ __global__ __launch_bounds__(512) void gemm256_mx_kernel(const uint8_t* __restri
           epi.put4x(row, n0 + ec, *(const float4*)(stg + lr * EPI_LD + ec), bv, xr[k]);
       }
     } else if (full) {
-#pragma unroll 4
+#pragma unroll
       for (int k = 0; k < 16; ++k) {
         const int lr = (tid >> 6) + 8 * k;
         const int row = m0 + (lr >> 6) * 128 + qi * 64 + (lr & 63);
