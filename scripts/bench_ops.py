@@ -57,8 +57,10 @@ def main():
         bias = torch.randn(4 * W, device="cuda", generator=g) * 0.02
         C16 = torch.empty(M, 4 * W, device="cuda", dtype=dt)
         X = torch.randn(M, W, device="cuda", generator=g)
-        shapes = [("qkv", 3 * W, W, 0, 0), ("out", W, W, 1, 0), ("fc", 4 * W, W, 0, 1),
-                  ("proj", W, 4 * W, 1, 0)]
+        X16 = X.half()
+        # out / proj: epilogue 4 = the fp16 residual stream of the fp16 model
+        shapes = [("qkv", 3 * W, W, 0, 0), ("out", W, W, 4, 0), ("fc", 4 * W, W, 0, 1),
+                  ("proj", W, 4 * W, 4, 0)]
         if args.ksweep:
             shapes = [(f"k{k}_e{e}", 4 * W, k, e, 0) for e in (3, 0, 2) for k in (256, 1024, 4096)]
         if args.only:
@@ -71,7 +73,7 @@ def main():
                  for x in args.variants.split(",")]
         for v in vlist:
             for name, N, K, epi, act in shapes:
-                C = X if epi == 1 else C16
+                C = X if epi == 1 else (X16 if epi == 4 else C16)
 
                 def fn():
                     rc = lib.miclip_op_gemm(0, A.data_ptr(), Wt.data_ptr(), bias.data_ptr(), C.data_ptr(),
@@ -79,7 +81,7 @@ def main():
                     assert rc == 0, lib.miclip_last_error()
                 ms = timeit(fn, args.iters)
                 fl = 2.0 * M * N * K
-                by = 2.0 * M * K + 2.0 * N * K + {0: 2.0, 1: 8.0, 2: 4.0, 3: 0.0}[epi] * M * N
+                by = 2.0 * M * K + 2.0 * N * K + {0: 2.0, 1: 8.0, 2: 4.0, 3: 0.0, 4: 4.0}[epi] * M * N
                 out.append(dict(op=f"gemm_{name}", variant=(f"{v & 0xffff}" + "".join(c for c, b in suffix.items() if v & b) if v >> 16 else v), M=M, N=N, K=K, ms=round(ms, 4),
                                 tflops=round(fl / ms / 1e9, 1), gbs=round(by / ms / 1e6, 1)))
                 print(json.dumps(out[-1]), flush=True)
@@ -92,7 +94,7 @@ def main():
                                 tflops=round(fl / ms / 1e9, 1)))
                 print(json.dumps(out[-1]), flush=True)
                 del a_, w_
-        del A, Wt, C16, X
+        del A, Wt, C16, X, X16
     if "attention" in args.ops:
         dh = args.head_dim
         H = W // dh
