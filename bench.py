@@ -177,12 +177,15 @@ def main():
         model.set_splits(args.splits)
 
     roofline, kernels = None, None
-    if rank == 0 and not args.no_profile:
+    prof = None
+    if not args.no_profile:
+        # every rank runs the profiled step: it contains the all-gather
         model.set_profiling(True)
         step()
         torch.cuda.synchronize()
         prof = model.profile_read(reset=True)
         model.set_profiling(False)
+    if rank == 0 and prof is not None:
         kernels = {k: dict(launches=v["launches"], ms=round(v["ms"], 4),
                            tflops=round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1) if v["flops"] else None,
                            gbs=round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1))
