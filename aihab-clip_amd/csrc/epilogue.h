@@ -119,6 +119,7 @@ struct EpiStore {
   T* C;
   const float* bias;
   int ldc;
+  int nt = 0;   // non-temporal output stores (MICLIP_GEMM_NT, A/B diagnostic)
   MICLIP_DEV float4 bias4(int col) const { return ld_bias4(bias, col); }
   MICLIP_DEV float4 bias4nb(int col) const { return ld_bias4_nb(bias, col); }
   MICLIP_DEV float bias1(int col) const { return bias ? bias[col] : 0.f; }
@@ -150,6 +151,8 @@ struct EpiStore {
     }
     if constexpr (ASM)
       st_b64_asm(C + (size_t)r * ldc + c, o);
+    else if (nt)
+      __builtin_nontemporal_store(o, (i16x4*)(C + (size_t)r * ldc + c));
     else
       *(i16x4*)(C + (size_t)r * ldc + c) = o;
   }

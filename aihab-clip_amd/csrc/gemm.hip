@@ -1236,16 +1236,26 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
 
 }  // namespace
 
+// MICLIP_GEMM_NT=1: non-temporal stores of the GEMM output (A/B diagnostic)
+int gemm_nt() {
+  static int v = [] {
+    const char* e = getenv("MICLIP_GEMM_NT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 template <typename T>
 hipError_t gemm_store_t(const void* A, const void* W, const float* bias, void* C, int M, int N,
                         int K, int act, hipStream_t s, int v) {
+  const int nt = gemm_nt();
   switch (act) {
     case ACT_NONE:
-      return launch<T>(A, W, M, N, K, EpiStore<T, ACT_NONE>{(T*)C, bias, N}, s, v);
+      return launch<T>(A, W, M, N, K, EpiStore<T, ACT_NONE>{(T*)C, bias, N, nt}, s, v);
     case ACT_QUICKGELU:
-      return launch<T>(A, W, M, N, K, EpiStore<T, ACT_QUICKGELU>{(T*)C, bias, N}, s, v);
+      return launch<T>(A, W, M, N, K, EpiStore<T, ACT_QUICKGELU>{(T*)C, bias, N, nt}, s, v);
     case ACT_GELU:
-      return launch<T>(A, W, M, N, K, EpiStore<T, ACT_GELU>{(T*)C, bias, N}, s, v);
+      return launch<T>(A, W, M, N, K, EpiStore<T, ACT_GELU>{(T*)C, bias, N, nt}, s, v);
     default:
       return hipErrorInvalidValue;
   }
