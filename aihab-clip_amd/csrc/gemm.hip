@@ -753,6 +753,255 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
 
 
 // ---------------------------------------------------------------------------
+// Persistent staggered kernel with the LDS-staged epilogue (variant 259). One
+// workgroup per CU walks tiles blockIdx.x + i*gridDim.x (the same XCD-grouped
+// rounds as the one-tile-per-workgroup launch); per tile the main loop is
+// SCHED 2 unchanged. What changes is the tile boundary:
+//   * the epilogue stages 64 accumulator rows per pass (4 passes) in the
+//     buffer-1 half of LDS, so buffer 0 is free: right after the main loop the
+//     next tile's whole first K-tile is LDS-DMA'd into it (hidden from hipcc,
+//     so it does not wait vmcnt(0) before the staging ds_reads), under the
+//     epilogue;
+//   * the workgroup does not end after its stores: they drain while the next
+//     tile's main loop starts (a retiring wave waits for its stores).
+// At the next tile: K-tile 1 is staged into buffer 1 (freed by the last pass's
+// barrier) and `vmcnt(4 + stores)` retires the prefetched K-tile 0 -- `stores`
+// is the epilogue's global stores per lane after the prefetch (32 for a full
+// tile; 0 for a partial tile, i.e. a full wait), never more than were issued.
+// The row tail runs at the end on the same workgroups (gemm_tail_wg tasks).
+// ---------------------------------------------------------------------------
+template <class Epi> struct EpiStores { static constexpr int n = 32; };   // 4 passes x 8 rows
+template <> struct EpiStores<EpiNull> { static constexpr int n = 0; };
+
+MICLIP_DEV void wait_vmcnt_tile(int n) {
+  switch (n) {
+    case 36: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
+    case 32: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+template <typename T, class Epi>
+__global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
+                                                       const T* __restrict__ W, int M, int N,
+                                                       int K, Epi epi, int gm, int ntm_dp,
+                                                       int ntail, int tail_wide) {
+  constexpr int HALF = 128 * 128;        // bytes of one half-tile slot
+  constexpr int EPI_LD = 260;            // fp32 row stride of the epilogue staging
+  constexpr int STG = 4 * HALF;          // staging: 64 rows in the buffer-1 half onward
+  constexpr int SMEM = 8 * HALF > STG + 64 * EPI_LD * 4 ? 8 * HALF : STG + 64 * EPI_LD * 4;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const int ntn = N / 256, ntm = ntm_dp, ndp = ntm * ntn, nk = K / 64;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int lchunk = (lane & 7) ^ (lane >> 3);
+  const int fr = lane & 15, fk = lane >> 4;
+  const int aoff = (wr * 64 + fr) * 128, boff = (wc * 32 + fr) * 128;
+  const int sw0 = ((0 + fk) ^ (fr & 7)) << 4, sw1 = ((4 + fk) ^ (fr & 7)) << 4;
+  const int ec = (tid & 63) * 4;
+
+  // LDS-DMA sources of tile `id` (slot row sr = piece*8 + (lane>>3))
+  auto sources = [&](int id, int& m0_, int& n0_, const T* (&as)[2][2], const T* (&bs)[2][2]) {
+    int tm_, tn_;
+    group_tile(xcd_remap(id, ndp), ntm, ntn, gm, tm_, tn_);
+    m0_ = tm_ * 256;
+    n0_ = tn_ * 256;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        const int sr = (wave * 2 + pp) * 8 + (lane >> 3);
+        int ar = m0_ + (sr >> 6) * 128 + h * 64 + (sr & 63);
+        ar = ar < M ? ar : M - 1;
+        as[h][pp] = A + (size_t)ar * K + lchunk * 8;
+        const int bc = n0_ + (sr >> 5) * 64 + h * 32 + (sr & 31);
+        bs[h][pp] = W + (size_t)bc * K + lchunk * 8;
+      }
+  };
+  int m0, n0;
+  const T* asrc[2][2];
+  const T* bsrc[2][2];
+  auto stage = [&](int slot_kind, int tile) {
+    const int buf = tile & 1, k0 = tile * 64;
+    char* dst = smem + (buf * 4 + slot_kind) * HALF + wave * 2048;
+    const T* const* src = slot_kind < 2 ? asrc[slot_kind] : bsrc[slot_kind - 2];
+    glds16(src[0] + k0, dst);
+    glds16(src[1] + k0, dst + 1024);
+  };
+
+  f32x4 acc[2][2][4][2];
+  i16x8 af[2][4], bf[2][2];
+  auto quadrant = [&](const char* sa, const char* sb, bool load_a) {
+    if (load_a) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        af[0][i] = *(const i16x8*)(sa + i * 2048 + sw0);
+        af[1][i] = *(const i16x8*)(sa + i * 2048 + sw1);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bf[0][j] = *(const i16x8*)(sb + j * 2048 + sw0);
+      bf[1][j] = *(const i16x8*)(sb + j * 2048 + sw1);
+    }
+  };
+  auto mfma_q = [&](int qi, int qj) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[qi][qj][i][j] = Mfma<T>::m16(af[s][i], bf[s][j], acc[qi][qj][i][j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  int prev_stores = -1;   // -1: first tile (full prologue)
+  int id = blockIdx.x;
+  if (id < ndp) sources(id, m0, n0, asrc, bsrc);
+  for (; id < ndp; id += gridDim.x) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (prev_stores < 0) {
+      stage(0, 0);
+      stage(3, 0);
+      stage(1, 0);
+      stage(2, 0);
+      stage(0, 1);
+      stage(3, 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      // K-tile 0 was prefetched during the previous epilogue
+      stage(0, 1);
+      stage(3, 1);
+      wait_vmcnt_tile(4 + prev_stores);
+    }
+    lds_barrier();
+    if (wr == 1) lds_barrier();   // stagger (wave-uniform)
+    for (int t = 0; t < nk; ++t) {
+      const int buf = t & 1;
+      const char* sA0 = smem + (buf * 4 + 0) * HALF + aoff;
+      const char* sA1 = smem + (buf * 4 + 1) * HALF + aoff;
+      const char* sB0 = smem + (buf * 4 + 2) * HALF + boff;
+      const char* sB1 = smem + (buf * 4 + 3) * HALF + boff;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        if (p == 0 && wr == 0 && t > 0) {
+          if (t + 1 < nk)
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (p == 3 && wr == 1 && t + 1 < nk) {
+          if (t + 2 < nk)
+            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        const int qi = (p >= 2) ? 1 : 0;
+        const int qj = (p == 1 || p == 2) ? 1 : 0;
+        quadrant(qi ? sA1 : sA0, qj ? sB1 : sB0, p == 0 || p == 2);
+        if (p == 0 && t + 1 < nk) stage(1, t + 1);
+        if (p == 1 && t + 1 < nk) stage(2, t + 1);
+        if (p == 2 && t + 2 < nk) stage(0, t + 2);
+        if (p == 3 && t + 2 < nk) stage(3, t + 2);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        lds_barrier();
+        mfma_q(qi, qj);
+        lds_barrier();
+      }
+    }
+    if (wr == 0) lds_barrier();   // balance the stagger barrier
+
+    // ---- tile boundary: prefetch the next tile's K-tile 0 into buffer 0 ----
+    lds_barrier();                 // every wave is done with both buffers
+    const int cm0 = m0, cn0 = n0;
+    // the bias is loaded and retired here, before anything is in flight: a
+    // load left pending on some path makes hipcc wait vmcnt(0) at the next
+    // tile's first MFMA that reuses its registers (draining the prefetch/stores)
+    const float4 bv = epi.bias4nb(cn0 + ec);   // branch-free (null bias -> zeros)
+    asm volatile("" ::"v"(bv.x), "v"(bv.y), "v"(bv.z), "v"(bv.w));
+    const int nid = id + gridDim.x;
+    if (nid < ndp) {
+      sources(nid, m0, n0, asrc, bsrc);
+#pragma unroll
+      for (int kind = 0; kind < 4; ++kind) {
+        const T* const* src = kind < 2 ? asrc[kind] : bsrc[kind - 2];
+        char* dst = smem + kind * HALF + wave * 2048;
+        glds16_hidden(src[0], dst);
+        glds16_hidden(src[1], dst + 1024);
+      }
+    }
+    // ---- epilogue: 4 passes of 64 rows staged at STG ----
+    float* stg = (float*)(smem + STG);
+    const bool full = cm0 + 256 <= M;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      if (p > 0) lds_barrier();
+      i16x4 xr[8];
+      if constexpr (PrefetchX<Epi>::value) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int row = cm0 + p * 64 + (tid >> 6) + 8 * k;
+          xr[k] = epi.load4(row < M ? row : M - 1, cn0 + ec);
+        }
+      }
+      if (wr == (p >> 1)) {
+#pragma unroll
+        for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int lr = i * 16 + fk * 4 + r;               // 0..63
+                const int lc = wc * 64 + qj * 32 + j * 16 + fr;   // 0..255
+                stg[lr * EPI_LD + lc] = acc[p & 1][qj][i][j][r];
+              }
+      }
+      lds_barrier();
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int lr = (tid >> 6) + 8 * k;
+        const int row = cm0 + p * 64 + lr;
+        if (full || row < M) {
+          const float4 v = *(const float4*)(stg + lr * EPI_LD + ec);
+          if constexpr (PrefetchX<Epi>::value)
+            epi.put4x(row, cn0 + ec, v, bv, xr[k]);
+          else
+            epi.put4(row, cn0 + ec, v, bv);
+        }
+      }
+      if constexpr (PrefetchX<Epi>::value) {   // retire every residual load on every path
+#pragma unroll
+        for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(xr[k]));
+      }
+    }
+    lds_barrier();                 // staging (buffer-1 half) free for the next tile
+    prev_stores = full ? EpiStores<Epi>::n : 0;
+  }
+  // the row tail on the same workgroups
+  for (int task = blockIdx.x; task < ntail; task += gridDim.x) {
+    lds_barrier();
+    if (tail_wide)
+      gemm_tail_wg<T, Epi, 2, 128>(A, W, M, N, K, epi, ntm * 256, task, smem);
+    else
+      gemm_tail_wg<T, Epi, 1, 64>(A, W, M, N, K, epi, ntm * 256, task, smem);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Persistent form of the staggered 256x256 kernel (SCHED 2): one workgroup per
 // CU walks its tiles (ids blockIdx.x + i*gridDim.x, so every round covers the
 // same XCD-grouped tile range as the one-tile-per-workgroup launch) as ONE
@@ -1171,8 +1420,23 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   variant %= 1000;
   if (variant == 0) variant = gemm_variant();
   if (variant != 0 && variant != 128 && variant != 256 && variant != 257 && variant != 258 &&
-      variant != 260 && variant != 2 && variant != 3)
+      variant != 259 && variant != 260 && variant != 2 && variant != 3)
     return hipErrorInvalidValue;
+  // default for full-size problems: the persistent staggered kernel (variant
+  // 259; same-process A/B vs 258 on the ViT-L/14 shapes: QKV +1 %, out-proj +9 %,
+  // c_fc +1 %, c_proj +1 %)
+  if (variant == 0 && !IsPatch<Epi>::value && N % 256 == 0 && K >= 128 &&
+      ((M + 255) / 256) * (N / 256) >= cu_count())
+    variant = 259;
+  if (variant == 259 && !IsPatch<Epi>::value && N % 256 == 0 && K >= 128) {
+    // persistent staggered kernel, LDS-staged epilogue + next-tile prefetch
+    const TailPlan tp = notail ? TailPlan{(M + 255) / 256, 0, 0} : plan_tail(M, N);
+    const int ndp = tp.ntm_dp * (N / 256), ncu = cu_count();
+    const int grid = ndp < ncu ? ndp : ncu;
+    hipLaunchKernelGGL((gemm256s_kernel<T, Epi>), dim3(grid), dim3(512), 0, s, (const T*)A,
+                       (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs, tp.wide & 1);
+    return hipGetLastError();
+  }
   if (variant == 3) {   // persistent 256x256
     const int ncu = cu_count();
     const int tiles = ((M + 255) / 256) * (N / 256);

@@ -42,7 +42,10 @@ def _check(lib, rc):
                                           (1000, 768, 3072, 258), (300, 256, 192, 258), (257, 512, 64, 258),
                                           (4096, 1024, 1024, 258), (33, 2304, 128, 258),
                                           (1000, 768, 3072, 260), (300, 256, 192, 260), (257, 512, 64, 260),
-                                          (4096, 1024, 1024, 260), (33, 2304, 128, 260)])
+                                          (4096, 1024, 1024, 260), (33, 2304, 128, 260),
+                                          (1000, 768, 3072, 259), (300, 256, 192, 259), (257, 512, 64, 259),
+                                          (4096, 1024, 1024, 259), (33, 2304, 128, 259),
+                                          (65792, 1024, 1024, 259), (16448, 3072, 256, 259)])
 @pytest.mark.parametrize("epi,act", [(0, 0), (0, 1), (0, 2), (1, 0), (2, 0), (4, 0)])
 def test_gemm(lib, dt, M, N, K, variant, epi, act):
     code, tdt = DT[dt]
@@ -87,7 +90,7 @@ NO_TAIL = 1 << 16   # gemm.hip kGemmNoTail: every row in 256x256 tiles
 @pytest.mark.parametrize("M,N,K", [(16448, 1024, 1024), (16421, 1024, 256), (4112, 4096, 512),
                                    (16448, 3072, 256), (16500, 1024, 2048), (4352, 4096, 512),
                                    (4296, 4096, 256), (16640, 3072, 256)])
-@pytest.mark.parametrize("variant", [258, 260, 256, 258 | (1 << 17), 260 | (1 << 17)])
+@pytest.mark.parametrize("variant", [258, 260, 256, 258 | (1 << 17), 260 | (1 << 17), 259])
 @pytest.mark.parametrize("epi,act", [(0, 0), (0, 1), (0, 2), (1, 0), (2, 0), (4, 0)])
 def test_gemm_tail_bitexact(lib, dt, M, N, K, variant, epi, act):
     """Row tail of a 256x256 launch (rows past the last whole round of tiles,
