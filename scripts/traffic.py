@@ -28,7 +28,7 @@ def launches(path, counter):
     rows = []
     with open(path) as f:
         for r in csv.DictReader(f):
-            if (r["Counter_Name"] == counter and "gemm256_kernel" in r["Kernel_Name"]
+            if (r["Counter_Name"] == counter and ("gemm256_kernel" in r["Kernel_Name"] or "gemm256s_kernel" in r["Kernel_Name"])
                     and "EpiStore" in r["Kernel_Name"] and "Li1EE" in r["Kernel_Name"]):
                 rows.append((int(r["Grid_Size"]), float(r["Counter_Value"])))
     if not rows:
