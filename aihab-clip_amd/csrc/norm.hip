@@ -119,11 +119,15 @@ MICLIP_DEV float half_sum(float x) {
   return x + __shfl_xor(x, 16, 64);
 }
 
-template <int NI, typename T>
+// MX = true: MX-fp8 output (the fp8 GEMM's A operand) instead of T; a 32-value
+// block is the 4 lanes of a quad here (8 values per lane), scale by lane 0 of it.
+template <int NI, typename T, bool MX>
 __global__ __launch_bounds__(256) void layernorm_h2_kernel(const _Float16* in,  // may alias out
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ beta,
-                                                           T* out, int R, int D) {
+                                                           T* out, int R, int D,
+                                                           uint8_t* __restrict__ oq,
+                                                           uint8_t* __restrict__ os) {
   const int lane = threadIdx.x & 63, hl = lane & 31;
   const int r = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
   if ((blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 >= R) return;   // whole wave past the end
@@ -155,20 +159,40 @@ __global__ __launch_bounds__(256) void layernorm_h2_kernel(const _Float16* in,  
     const float4 b0 = *(const float4*)(beta + c), b1 = *(const float4*)(beta + c + 4);
     const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
     const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-    i16x8 o;
+    if constexpr (MX) {
+      float y[8];
+      float a = 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = to_bits<T>(v[i][e] * rstd * g[e] + b[e]);
-    if (valid) *(i16x8*)(out + (size_t)r * D + c) = o;
+      for (int e = 0; e < 8; ++e) {
+        y[e] = v[i][e] * rstd * g[e] + b[e];
+        a = fmaxf(a, fabsf(y[e]));
+      }
+      a = fmaxf(a, dppf<0xB1>(a));   // quad_perm [1,0,3,2]
+      a = fmaxf(a, dppf<0x4E>(a));   // quad_perm [2,3,0,1]: the quad's 32 values
+      const int ex = mx_exponent(a);
+      const unsigned lo = mx_pack4(make_float4(y[0], y[1], y[2], y[3]), ex);
+      const unsigned hi = mx_pack4(make_float4(y[4], y[5], y[6], y[7]), ex);
+      if (valid) {
+        *(uint2*)(oq + (size_t)r * D + c) = make_uint2(lo, hi);
+        if ((hl & 3) == 0) os[mx_scale_index(r, c >> 5, D / 128)] = (uint8_t)(ex + 127);
+      }
+    } else {
+      i16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = to_bits<T>(v[i][e] * rstd * g[e] + b[e]);
+      if (valid) *(i16x8*)(out + (size_t)r * D + c) = o;
+    }
   }
 }
 
-template <typename T>
+template <typename T, bool MX = false>
 hipError_t ln_h2_dispatch(const _Float16* in, const float* g, const float* b, void* out, int R,
-                          int D, hipStream_t s) {
+                          int D, hipStream_t s, void* oq = nullptr, void* os = nullptr) {
   const dim3 grid((R + 7) / 8), block(256);
-#define MICLIP_LNH_CASE(V)                                                                       \
-  case V:                                                                                        \
-    hipLaunchKernelGGL((layernorm_h2_kernel<V, T>), grid, block, 0, s, in, g, b, (T*)out, R, D); \
+#define MICLIP_LNH_CASE(V)                                                                     \
+  case V:                                                                                      \
+    hipLaunchKernelGGL((layernorm_h2_kernel<V, T, MX>), grid, block, 0, s, in, g, b, (T*)out, \
+                       R, D, (uint8_t*)oq, (uint8_t*)os);                                      \
     break;
   switch (D / 256) {
     MICLIP_LNH_CASE(1)
@@ -220,6 +244,9 @@ hipError_t layernorm(int dtype, const void* in, const int32_t* rows, int in_stri
     if (dtype != kF16) return hipErrorInvalidValue;
     if (out_t && !out_f32 && !out_q && !rows && in_stride_rows == 1 && !normalize)
       return ln_h2_dispatch<_Float16>((const _Float16*)in, gamma, beta, out_t, R, D, s);
+    if (out_q && !out_f32 && !out_t && !rows && in_stride_rows == 1 && !normalize)
+      return ln_h2_dispatch<_Float16, true>((const _Float16*)in, gamma, beta, nullptr, R, D, s,
+                                            out_q, out_s);
     return ln_dispatch<_Float16>((const _Float16*)in, rows, in_stride_rows, gamma, beta, out_f32,
                                  out_t, R, D, normalize, s, oq, os);
   }
