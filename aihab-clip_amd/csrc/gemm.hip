@@ -1425,8 +1425,10 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   // default for full-size problems: the persistent staggered kernel (variant
   // 259; same-process A/B vs 258 on the ViT-L/14 shapes: QKV +1 %, out-proj +9 %,
   // c_fc +1 %, c_proj +1 %)
+  // (from half a round of 256x256 tiles up: ViT-B/32 bs=128 QKV 225 tiles 0.047 ->
+  // 0.028 ms, out-proj bs=256 150 tiles 0.051 -> 0.028 ms vs the 128x128 kernel)
   if (variant == 0 && !IsPatch<Epi>::value && N % 256 == 0 && K >= 128 &&
-      ((M + 255) / 256) * (N / 256) >= cu_count())
+      2 * ((M + 255) / 256) * (N / 256) >= cu_count())
     variant = 259;
   if (variant == 259 && !IsPatch<Epi>::value && N % 256 == 0 && K >= 128) {
     // persistent staggered kernel, LDS-staged epilogue + next-tile prefetch
@@ -1458,7 +1460,7 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   // Large problems: 256x256 tile (1 WG/CU, L2-friendly arithmetic intensity);
   // small ones (text tower, tiny batches) keep more workgroups with 128x128.
   const int tiles256 = ((M + 255) / 256) * (N / 256);
-  if (N % 256 == 0 && variant != 128 && (tiles256 >= 256 || variant >= 256)) {
+  if (N % 256 == 0 && variant != 128 && (2 * tiles256 >= cu_count() || variant >= 256)) {
     // default: the staggered schedule (SCHED 2) with the LDS-staged epilogue
     // (full 512-B / 1-KiB row stores) for every epilogue; 260 = the register
     // epilogue, 256 / 257 = SCHED 0 / 1. (The fp32 residual register epilogue
