@@ -196,6 +196,12 @@ struct EpiResidual {
   // rows are loaded (load4) before the accumulators are staged, so their latency
   // hides under the LDS writes instead of sitting in front of every store.
   MICLIP_DEV i16x4 load4(int r, int c) const { return *(const i16x4*)(X + (size_t)r * ldx + c); }
+  // fp32 stream (bf16 models): the same split form for the persistent kernel
+  MICLIP_DEV f32x4 load4f(int r, int c) const { return *(const f32x4*)(X + (size_t)r * ldx + c); }
+  MICLIP_DEV void put4xf(int r, int c, float4 v, float4 b, f32x4 x) const {
+    *(f32x4*)(X + (size_t)r * ldx + c) =
+        f32x4{x[0] + (v.x + b.x), x[1] + (v.y + b.y), x[2] + (v.z + b.z), x[3] + (v.w + b.w)};
+  }
   template <bool ASM = false>
   MICLIP_DEV void put4x(int r, int c, float4 v, float4 b, i16x4 x) const {
     i16x4 o;
@@ -222,6 +228,10 @@ struct EpiResidual {
 // staged epilogues prefetch those reads (load4 / put4x).
 template <class Epi> struct PrefetchX : std::false_type {};
 template <> struct PrefetchX<EpiResidual<_Float16>> : std::true_type {};
+// fp32 residual rows (16 B per lane) are prefetched by the persistent kernel only
+// (8 rows per pass; the one-tile kernel's 16 would cost 64 VGPRs)
+template <class Epi> struct PrefetchXF : std::false_type {};
+template <> struct PrefetchXF<EpiResidual<float>> : std::true_type {};
 
 struct EpiF32 {
   float* C;

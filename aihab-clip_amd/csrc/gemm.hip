@@ -949,11 +949,19 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
     for (int p = 0; p < 4; ++p) {
       if (p > 0) lds_barrier();
       i16x4 xr[8];
+      f32x4 xf[8];
       if constexpr (PrefetchX<Epi>::value) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const int row = cm0 + p * 64 + (tid >> 6) + 8 * k;
           xr[k] = epi.load4(row < M ? row : M - 1, cn0 + ec);
+        }
+      }
+      if constexpr (PrefetchXF<Epi>::value) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int row = cm0 + p * 64 + (tid >> 6) + 8 * k;
+          xf[k] = epi.load4f(row < M ? row : M - 1, cn0 + ec);
         }
       }
       if (wr == (p >> 1)) {
@@ -979,6 +987,8 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
           const float4 v = *(const float4*)(stg + lr * EPI_LD + ec);
           if constexpr (PrefetchX<Epi>::value)
             epi.put4x(row, cn0 + ec, v, bv, xr[k]);
+          else if constexpr (PrefetchXF<Epi>::value)
+            epi.put4xf(row, cn0 + ec, v, bv, xf[k]);
           else
             epi.put4(row, cn0 + ec, v, bv);
         }
@@ -986,6 +996,10 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
       if constexpr (PrefetchX<Epi>::value) {   // retire every residual load on every path
 #pragma unroll
         for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(xr[k]));
+      }
+      if constexpr (PrefetchXF<Epi>::value) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(xf[k]));
       }
     }
     lds_barrier();                 // staging (buffer-1 half) free for the next tile
