@@ -15,7 +15,7 @@ all: $(LIB)
 
 # attention: no NaN inputs by construction (masked scores are -inf), so fmaxf
 # needs no per-operand canonicalising v_max (20 -> 7 v_max per key tile)
-$(OBJ_DIR)/attention.o: HIPFLAGS += -fno-honor-nans
+$(OBJ_DIR)/attention.o: HIPFLAGS += -fno-honor-nans -fno-slp-vectorize
 
 $(OBJ_DIR)/%.o: $(SRC_DIR)/%.hip $(HDRS)
 	@mkdir -p $(OBJ_DIR)
