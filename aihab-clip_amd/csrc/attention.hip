@@ -66,7 +66,7 @@ template <typename T, bool CAUSAL, int DH>
 MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
                              const i16x8 (&qf)[HeadGeom<DH>::NKS], int chunk, int N, int Npad,
                              float c2, int lane, f32x16 (&o)[HeadGeom<DH>::NDT], float& lsum,
-                             float& m, int kt0 = 0, int kt_end = -1) {
+                             float& m, int kt0 = 0, int kt_end = -1, int prio = 0) {
   using G = HeadGeom<DH>;
   const int l32 = lane & 31, hh = lane >> 5;
   const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
@@ -102,11 +102,13 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
     const char* ktile = kimg + kt * G::TILEB;
 #pragma unroll
     for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+    if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < G::NKS; ++s) {
       const i16x8 kf = *(const i16x8*)(ktile + koff[s]);
       sacc = Mfma<T>::m32(kf, qf[s], sacc);
     }
+    if (prio) __builtin_amdgcn_s_setprio(0);
   };
   auto softmax_pv = [&](int kt, f32x16& sacc) {
     const char* vtile = vimg + kt * G::TILEB;
@@ -161,6 +163,7 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
 #pragma unroll
       for (int j = 0; j < 8; ++j) pf[s2][j] = to_bits<T>(sacc[8 * s2 + j]);
     // ---- O^T[d][q] += V^T . P^T ----
+    if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
 #pragma unroll
@@ -173,6 +176,7 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
         o[dt] = Mfma<T>::m32(vf, pf[s2], o[dt]);
       }
     }
+    if (prio) __builtin_amdgcn_s_setprio(0);
   };
   f32x16 sa, sb;
   int kt = kt0;
@@ -231,7 +235,7 @@ MICLIP_DEV void load_q(i16x8 (&qf)[HeadGeom<DH>::NKS], const T* base, int ld, in
 template <typename T, bool CAUSAL, int DH>
 __global__ __launch_bounds__(DH == 64 ? 640 : 576) void attention_kernel(
     const T* __restrict__ qkv, T* __restrict__ out, int N, int H, int Npad, int nchunks,
-    float qk_scale) {
+    float qk_scale, int prio) {
   using G = HeadGeom<DH>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* kimg = smem;                  // [Npad][ROWB/2] T
@@ -261,7 +265,8 @@ __global__ __launch_bounds__(DH == 64 ? 640 : 576) void attention_kernel(
     load_q<T, DH>(qf, base, ld, chunk, N, lane);
     f32x16 o[G::NDT];
     float lsum, m;
-    attend_chunk<T, CAUSAL, DH>(kimg, vimg, qf, chunk, N, Npad, c2, lane, o, lsum, m);
+    attend_chunk<T, CAUSAL, DH>(kimg, vimg, qf, chunk, N, Npad, c2, lane, o, lsum, m, 0, -1,
+                                prio);
     attend_store<T, DH>(o, lsum, chunk, N, out + (size_t)b * N * D + h * DH, D, lane);
   }
 }
@@ -288,7 +293,7 @@ __global__ __launch_bounds__(DH == 64 ? 640 : 576) void attention_kernel(
 template <typename T, bool CAUSAL, bool SPLIT>
 __global__ __launch_bounds__(SPLIT ? 512 : 640) void attention_pipe_kernel(
     const T* __restrict__ qkv, T* __restrict__ out, int B, int N, int H, int Npad, int hpw,
-    float qk_scale) {
+    float qk_scale, int prio) {
   constexpr bool split = SPLIT;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int img_bytes = Npad * 128;            // one K or V image
@@ -370,7 +375,8 @@ __global__ __launch_bounds__(SPLIT ? 512 : 640) void attention_pipe_kernel(
     const char* kimg = smem + (j & 1) * 2 * img_bytes;
     f32x16 o[2];
     float lsum, m;
-    attend_chunk<T, CAUSAL, 64>(kimg, kimg + img_bytes, qf, wave, N, Npad, c2, lane, o, lsum, m);
+    attend_chunk<T, CAUSAL, 64>(kimg, kimg + img_bytes, qf, wave, N, Npad, c2, lane, o, lsum, m,
+                                0, -1, prio);
     // Take head j+1's Q BEFORE this head's output stores: hipcc's wait for
     // the qn loads (which also retires the older DMA of head j+1) then never
     // waits for the stores, which drain under the next head's work.
@@ -423,6 +429,17 @@ int attn_variant() {
   return v;
 }
 
+// s_setprio 1 around each tile's MFMA issue: with 2-3 waves per SIMD the one
+// issuing MFMAs goes first, the others' softmax VALU fills its gaps (ViT-L/14
+// layer: 0.184 -> 0.177 ms, same-box A/B). MICLIP_ATTN_PRIO=0 turns it off.
+int attn_prio() {
+  static int v = [] {
+    const char* e = getenv("MICLIP_ATTN_PRIO");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 // MICLIP_ATTN_SPLIT=1 (or variant 4) spreads a 1-2-query last chunk over the
 // other waves. Off by default: at N = 257 it measured level with the 9-wave
 // form (0.183 vs 0.181 ms per ViT-L/14 layer at bs=256, same process).
@@ -455,7 +472,7 @@ hipError_t attn_launch_plain(const void* qkv, void* out, int B, int N, int H, hi
     attr_set = true;
   }
   hipLaunchKernelGGL(kern, dim3(B * H), dim3(nw * 64), lds, s, (const T*)qkv, (T*)out, N, H,
-                     Npad, nchunks, 1.0f / sqrtf((float)DH));
+                     Npad, nchunks, 1.0f / sqrtf((float)DH), attn_prio());
   return hipGetLastError();
 }
 
@@ -502,10 +519,12 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, 
     const int grid = (heads + hpw - 1) / hpw;
     if (split)
       hipLaunchKernelGGL((attention_pipe_kernel<T, CAUSAL, true>), dim3(grid), dim3(waves * 64),
-                         lds_all, s, (const T*)qkv, (T*)out, B, N, H, Npad, hpw, 0.125f);
+                         lds_all, s, (const T*)qkv, (T*)out, B, N, H, Npad, hpw, 0.125f,
+                         attn_prio());
     else
       hipLaunchKernelGGL((attention_pipe_kernel<T, CAUSAL, false>), dim3(grid), dim3(waves * 64),
-                         lds_all, s, (const T*)qkv, (T*)out, B, N, H, Npad, hpw, 0.125f);
+                         lds_all, s, (const T*)qkv, (T*)out, B, N, H, Npad, hpw, 0.125f,
+                         attn_prio());
     return hipGetLastError();
   }
   return attn_launch_plain<T, CAUSAL, 64>(qkv, out, B, N, H, s);
