@@ -1213,6 +1213,135 @@ __global__ __launch_bounds__(512) void gemm256p_kernel(const T* __restrict__ A,
   if (wr == 0) lds_barrier();   // balance the stagger barrier
 }
 // ---------------------------------------------------------------------------
+// 256x256 tile, 256 threads = 4 waves (2x2), 128x128 per wave: ONE wave per
+// SIMD, its 8x8 grid of 16x16 fp32 fragments (256 registers) in the AGPR half
+// of the register file. Per 32-k step a wave reads 16 fragments (8 A + 8 B)
+// for 64 MFMAs -- half the LDS bytes per flop of the 8-wave 128x64 layout --
+// and it issues those reads for the NEXT step and its share of the LDS-DMA
+// between its own MFMAs, so the matrix pipe is fed without a partner wave.
+// LDS: 4 stages x 32 KiB (A 256 rows + W 256 rows of 64 B = 32 k each);
+// 16-B chunk c of row r at physical chunk c ^ (((r >> 2) & 1) << 1)
+// (conflict-free ds_read_b128 fragment reads; checked with the lane-group
+// bank model). Stage t+3 is DMA'd during step t and retired (own vmcnt +
+// the one barrier per step) at the top of step t+2: two steps of latency
+// slack. Register epilogue (quad transpose -> put4), one tile per workgroup.
+// Variant 300, not a default: parity-green, but same-process A/B on the
+// ViT-L/14 bs=256 shapes it is 15-40 % slower than the persistent 8-wave
+// kernel (c_proj 0.677 vs 0.479 ms): the 256 accumulators fill the AGPR half
+// exactly and hipcc bounces a few through VGPRs every step, and 64-B rows
+// halve the bytes per DMA row request. Kept as the starting point for a
+// one-wave-per-SIMD schedule.
+// ---------------------------------------------------------------------------
+template <typename T, class Epi>
+__global__ __launch_bounds__(256, 1) void gemm4w_kernel(const T* __restrict__ A,
+                                                        const T* __restrict__ W, int M, int N,
+                                                        int K, Epi epi, int gm) {
+  constexpr int STAGE = 32 * 1024, NS = 4;
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int ntn = N / 256, ntm = (M + 255) / 256, nk = K / 32;
+  int tm, tn;
+  group_tile(xcd_remap(blockIdx.x, ntm * ntn), ntm, ntn, gm, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  // DMA pieces: 1 KiB = 16 rows x 64 B; stage piece p < 16: A rows 16p.., else
+  // W rows 16(p-16)..; wave w issues pieces 8w .. 8w+7 (waves 0-1 A, 2-3 W).
+  const int prow = lane >> 2;
+  const int lch = (lane & 3) ^ (((prow >> 2) & 1) << 1);
+  // one base pointer per lane + 32-bit row offsets (A rows clamped to M-1:
+  // finite duplicates of the last row, never stored)
+  const T* base = wave < 2 ? A + lch * 8 : W + (size_t)n0 * K + lch * 8;
+  unsigned roff[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int piece = (wave & 1) * 8 + p;
+    int r = piece * 16 + prow;
+    if (wave < 2) r = m0 + r < M ? m0 + r : M - 1;
+    roff[p] = (unsigned)r * (unsigned)K;
+  }
+  // stages past the last one re-fetch the last stage into a dead buffer, so
+  // every step issues exactly 8 DMAs per wave (branch-free, fixed vmcnt)
+  auto dma = [&](int kt, int p) {
+    kt = kt < nk ? kt : nk - 1;
+    glds16_hidden(base + roff[p] + kt * 32,
+                  smem + (kt & (NS - 1)) * STAGE + (wave * 8 + p) * 1024);
+  };
+  const int fr = lane & 15, fk = lane >> 4;
+  const int sw = (fk ^ (((fr >> 2) & 1) << 1)) << 4;
+  const int aoff = (wr * 128 + fr) * 64 + sw;
+  const int boff = 16384 + (wc * 128 + fr) * 64 + sw;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // A fragments single-buffered (fa[g] is reloaded for the next step right
+  // after group g's MFMAs, its last use), W fragments double-buffered (every
+  // group reads all 8): 96 fragment VGPRs next to the 256 AGPR accumulators
+  i16x8 fa[8], fb[2][8];
+
+  // prologue: stages 0..2 in flight, stage 0 retired, F(0) read
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int p = 0; p < 8; ++p) dma(s, p);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  lds_barrier();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    fa[i] = *(const i16x8*)(smem + aoff + i * 1024);
+    fb[0][i] = *(const i16x8*)(smem + boff + i * 1024);
+  }
+
+  auto step = [&](int t, auto par) {
+    constexpr int cur = decltype(par)::value, nxt = cur ^ 1;
+    // retire this wave's DMA of stage t+1 (8 younger: stage t+2's); the
+    // barrier makes every wave's visible and ends all reads of stage t-1's
+    // buffer (= stage t+3's). Past the last stage the reads and DMAs are
+    // harmless duplicates (dead buffers), so the step stays branch-free.
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    lds_barrier();
+    const char* nb = smem + ((t + 1) & (NS - 1)) * STAGE;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      dma(t + 3, g);
+      fb[nxt][g] = *(const i16x8*)(nb + boff + g * 1024);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[g][j] = Mfma<T>::m16(fa[g], fb[cur][j], acc[g][j]);
+      __builtin_amdgcn_s_setprio(0);
+      fa[g] = *(const i16x8*)(nb + aoff + g * 1024);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // K % 64 == 0 (launch check): steps come in pairs, one per register set
+  for (int t = 0; t < nk; t += 2) {
+    step(t, std::integral_constant<int, 0>{});
+    step(t + 1, std::integral_constant<int, 1>{});
+  }
+  // no LDS-DMA may land after the workgroup's LDS is handed to the next one
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // epilogue straight from the accumulators
+  const int q = (lane & 15) >> 2, jj = lane & 3;
+  float4 bv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bv[j] = epi.bias4nb(n0 + wc * 128 + j * 16 + 4 * q);
+  const bool full = m0 + 256 <= M;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = m0 + wr * 128 + i * 16 + fk * 4 + jj;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = n0 + wc * 128 + j * 16 + 4 * q;
+      const float4 v = quad_transpose(acc[i][j], lane);
+      if (full || row < M) epi.put4(row, col, v, bv[j]);
+    }
+  }
+}
+// ---------------------------------------------------------------------------
 // 256x128x32 tile, 256 threads = 4 waves as 2(M) x 2(N), 128x64 per wave,
 // three LDS stages of 24 KiB (72 KiB per workgroup) so TWO workgroups share a
 // CU: one workgroup's prologue/epilogue (HBM-burst bound) overlaps the other's
@@ -1434,8 +1563,17 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   variant %= 1000;
   if (variant == 0) variant = gemm_variant();
   if (variant != 0 && variant != 128 && variant != 256 && variant != 257 && variant != 258 &&
-      variant != 259 && variant != 260 && variant != 2 && variant != 3)
+      variant != 259 && variant != 260 && variant != 2 && variant != 3 && variant != 300)
     return hipErrorInvalidValue;
+  if constexpr (!IsPatch<Epi>::value) {
+    if (variant == 300 && N % 256 == 0 && K % 64 == 0) {
+      // 4-wave 128x128-per-wave kernel (A/B prototype), one tile per workgroup
+      const int tiles = ((M + 255) / 256) * (N / 256);
+      hipLaunchKernelGGL((gemm4w_kernel<T, Epi>), dim3(tiles), dim3(256), 0, s, (const T*)A,
+                         (const T*)W, M, N, K, epi, gm);
+      return hipGetLastError();
+    }
+  }
   // default for full-size problems: the persistent staggered kernel (variant
   // 259; same-process A/B vs 258 on the ViT-L/14 shapes: QKV +1 %, out-proj +9 %,
   // c_fc +1 %, c_proj +1 %)

@@ -45,7 +45,9 @@ def _check(lib, rc):
                                           (4096, 1024, 1024, 260), (33, 2304, 128, 260),
                                           (1000, 768, 3072, 259), (300, 256, 192, 259), (257, 512, 64, 259),
                                           (4096, 1024, 1024, 259), (33, 2304, 128, 259),
-                                          (65792, 1024, 1024, 259), (16448, 3072, 256, 259)])
+                                          (65792, 1024, 1024, 259), (16448, 3072, 256, 259),
+                                          (1000, 768, 3072, 300), (300, 256, 192, 300), (257, 512, 64, 300),
+                                          (65792, 1024, 1024, 300), (16448, 3072, 256, 300)])
 @pytest.mark.parametrize("epi,act", [(0, 0), (0, 1), (0, 2), (1, 0), (2, 0), (4, 0)])
 def test_gemm(lib, dt, M, N, K, variant, epi, act):
     code, tdt = DT[dt]
