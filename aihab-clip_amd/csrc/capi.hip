@@ -78,6 +78,10 @@ struct Block {
   float *ln1_g = nullptr, *ln1_b = nullptr, *ln2_g = nullptr, *ln2_b = nullptr;
   // MX-fp8 models: scale planes of w_qkv / w_fc / w_proj (which then hold e4m3 bytes)
   void *s_qkv = nullptr, *s_fc = nullptr, *s_proj = nullptr;
+  // folded LayerNorm (miclip_model::lnfold): W diag(gamma) of QKV / c_fc, their
+  // column sums and folded biases (epilogue.h EpiStoreLN)
+  void *wf_qkv = nullptr, *wf_fc = nullptr;
+  float *cs_qkv = nullptr, *c_qkv = nullptr, *cs_fc = nullptr, *c_fc = nullptr;
 };
 
 struct Workspace {
@@ -93,6 +97,7 @@ struct Workspace {
   void *hq = nullptr, *hs = nullptr, *fq = nullptr, *fs = nullptr;
   float* feat = nullptr;  // [items, W] fp32 scratch
   int32_t* rows = nullptr;
+  float* stats = nullptr;  // [rows] {mean, rstd} for the folded LayerNorm
 };
 
 }  // namespace
@@ -109,6 +114,11 @@ struct miclip_model {
   // MICLIP_MXFP8: QKV / c_fc / c_proj run on MX-fp8 operands (gemm_mx.hip);
   // everything else (patch embed, attention, out-proj, stream) as fp16 compute.
   bool mx = false;
+  // ln_1 / ln_2 folded into the QKV / c_fc GEMMs (fp16 stream models;
+  // MICLIP_LN_FOLD=0 runs the LayerNorm kernels instead); folded weights are
+  // rebuilt per tower after every weight load
+  int lnfold = 0;
+  bool folded[2] = {false, false};   // [visual, text]
   int Kp = 0;  // padded patch-GEMM K
   std::unordered_map<void*, size_t> allocs;
   int64_t bytes = 0;
@@ -256,7 +266,7 @@ int ensure_ws(miclip_model* m, Workspace& w, int items, int ntok, int W, bool im
   // grow: make sure no queued kernel still uses the old buffers
   MICLIP_HIP(hipDeviceSynchronize());
   for (void* p : {w.patches, (void*)w.x, w.h, w.qkv, w.o, w.f, w.hq, w.hs, w.fq, w.fs,
-                  (void*)w.feat, (void*)w.rows})
+                  (void*)w.feat, (void*)w.rows, (void*)w.stats})
     dev_free(m, p);
   w = Workspace{};
   int rc;
@@ -279,6 +289,7 @@ int ensure_ws(miclip_model* m, Workspace& w, int items, int ntok, int W, bool im
   }
   if ((rc = dev_alloc(m, (void**)&w.feat, (size_t)items * W * 4))) return rc;
   if ((rc = dev_alloc(m, (void**)&w.rows, (size_t)items * 4))) return rc;
+  if ((rc = dev_alloc(m, (void**)&w.stats, (size_t)rows * 8))) return rc;
   w.cap_items = items;
   w.cap_rows = rows;
   return 0;
@@ -291,12 +302,40 @@ double gemm_bytes(double M, double N, double K, double c_bytes) {
   return 2.0 * M * K + 2.0 * N * K + c_bytes * M * N;
 }
 
+// Build the folded QKV / c_fc weights of one tower (after every weight load).
+int ensure_folded(miclip_model* m, bool visual) {
+  if (!m->lnfold || m->folded[visual ? 0 : 1]) return 0;
+  const int W = visual ? m->cfg.vision_width : m->cfg.transformer_width;
+  int rc;
+  for (Block& b : visual ? m->vblocks : m->tblocks) {
+    if (!b.wf_qkv) {
+      if ((rc = dev_alloc(m, &b.wf_qkv, (size_t)3 * W * W * elt()))) return rc;
+      if ((rc = dev_alloc(m, &b.wf_fc, (size_t)4 * W * W * elt()))) return rc;
+      if ((rc = dev_alloc(m, (void**)&b.cs_qkv, (size_t)3 * W * 4))) return rc;
+      if ((rc = dev_alloc(m, (void**)&b.c_qkv, (size_t)3 * W * 4))) return rc;
+      if ((rc = dev_alloc(m, (void**)&b.cs_fc, (size_t)4 * W * 4))) return rc;
+      if ((rc = dev_alloc(m, (void**)&b.c_fc, (size_t)4 * W * 4))) return rc;
+    }
+    MICLIP_HIP(ln_fold(m->dtype, b.w_qkv, b.ln1_g, b.ln1_b, b.b_qkv, b.wf_qkv, b.cs_qkv, b.c_qkv,
+                       3 * W, W, nullptr));
+    MICLIP_HIP(ln_fold(m->dtype, b.w_fc, b.ln2_g, b.ln2_b, b.b_fc, b.wf_fc, b.cs_fc, b.c_fc,
+                       4 * W, W, nullptr));
+  }
+  MICLIP_HIP(hipDeviceSynchronize());
+  m->folded[visual ? 0 : 1] = true;
+  return 0;
+}
+
 int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, int W, int H,
               int dh, int causal, hipStream_t s) {
   const int M = items * N, dt = m->dtype, r16 = m->resid16;
   const double dM = M, dW = W, rb = r16 ? 2 : 4;  // residual bytes per element
   const bool mx = m->mx;   // MX-fp8 operands for QKV / c_fc / c_proj
-  {
+  const bool fold = m->lnfold && b.wf_qkv;
+  if (fold) {
+    ProfScope p(m, K_LAYERNORM, s, 0, dM * (dW * rb + 8));
+    MICLIP_HIP(ln_stats(w.x, w.stats, M, W, s));
+  } else {
     ProfScope p(m, K_LAYERNORM, s, 0, dM * dW * (rb + (mx ? 1 : 2)));
     if (mx)
       MICLIP_HIP(layernorm(dt, w.x, nullptr, 1, b.ln1_g, b.ln1_b, nullptr, nullptr, M, W, 0, s,
@@ -310,6 +349,9 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
     if (mx)
       MICLIP_HIP(gemm_mx(w.hq, w.hs, b.w_qkv, b.s_qkv, b.b_qkv, w.qkv, nullptr, M, 3 * W, W, 0,
                          ACT_NONE, s));
+    else if (fold)
+      MICLIP_HIP(gemm_store_ln(dt, w.x, b.wf_qkv, b.c_qkv, b.cs_qkv, w.stats, w.qkv, M, 3 * W, W,
+                               ACT_NONE, s));
     else
       MICLIP_HIP(gemm_store(dt, w.h, b.w_qkv, b.b_qkv, w.qkv, M, 3 * W, W, ACT_NONE, s));
   }
@@ -322,7 +364,10 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
     ProfScope p(m, K_GEMM_OUT, s, gemm_flops(dM, dW, dW), gemm_bytes(dM, dW, dW, 2 * rb));
     MICLIP_HIP(gemm_residual(dt, w.o, b.w_out, b.b_out, w.x, M, W, W, s, 0, r16));
   }
-  {
+  if (fold) {
+    ProfScope p(m, K_LAYERNORM, s, 0, dM * (dW * rb + 8));
+    MICLIP_HIP(ln_stats(w.x, w.stats, M, W, s));
+  } else {
     ProfScope p(m, K_LAYERNORM, s, 0, dM * dW * (rb + (mx ? 1 : 2)));
     if (mx)
       MICLIP_HIP(layernorm(dt, w.x, nullptr, 1, b.ln2_g, b.ln2_b, nullptr, nullptr, M, W, 0, s,
@@ -337,6 +382,9 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
     if (mx)
       MICLIP_HIP(gemm_mx(w.hq, w.hs, b.w_fc, b.s_fc, b.b_fc, w.fq, w.fs, M, 4 * W, W, 5,
                          m->cfg.act, s));
+    else if (fold)
+      MICLIP_HIP(gemm_store_ln(dt, w.x, b.wf_fc, b.c_fc, b.cs_fc, w.stats, w.f, M, 4 * W, W,
+                               m->cfg.act, s));
     else
       MICLIP_HIP(gemm_store(dt, w.h, b.w_fc, b.b_fc, w.f, M, 4 * W, W, m->cfg.act, s));
   }
@@ -376,6 +424,7 @@ Workspace view(const miclip_model* m, const Workspace& w, size_t row0, size_t it
   }
   v.feat = w.feat + item0 * W;
   v.rows = w.rows + item0;
+  v.stats = w.stats + 2 * row0;
   (void)N;
   return v;
 }
@@ -491,6 +540,8 @@ int miclip_model_create(const miclip_config* cfg, int device, miclip_model** out
   {
     const char* e = getenv("MICLIP_RESID_F32");
     m->resid16 = m->mx || (m->dtype == MICLIP_FP16 && !(e && atoi(e) != 0));
+    const char* f = getenv("MICLIP_LN_FOLD");
+    m->lnfold = !m->mx && m->resid16 && !(f && atoi(f) == 0);
   }
   const int P = cfg->vision_patch_size, Wv = cfg->vision_width, Wt = cfg->transformer_width;
   m->Kp = (3 * P * P + 63) / 64 * 64;
@@ -525,6 +576,7 @@ int miclip_model_create(const miclip_config* cfg, int device, miclip_model** out
 int miclip_model_load_weights(miclip_model* m, const miclip_tensor* t, int32_t n) {
   if (!m || (!t && n)) return fail(MICLIP_EINVAL, "null argument");
   MICLIP_HIP(hipSetDevice(m->device));
+  m->folded[0] = m->folded[1] = false;
   std::vector<uint16_t> tmp;
   for (int i = 0; i < n; ++i) {
     if (!t[i].name || !t[i].data) return fail(MICLIP_EINVAL, "null tensor name/data");
@@ -604,6 +656,7 @@ int miclip_encode_image(miclip_model* m, const float* images, int32_t B, float* 
   if (!m || !images || !out || B < 1) return fail(MICLIP_EINVAL, "bad argument to encode_image");
   if (!tower_loaded(m, true))
     return fail(MICLIP_ENOWEIGHTS, "visual weights not loaded (missing " + missing(m, true) + ")");
+  if (int rc0 = ensure_folded(m, true)) return rc0;
   hipStream_t s = (hipStream_t)stream;
   const auto& c = m->cfg;
   const int R = c.image_resolution, W = c.vision_width;
@@ -650,6 +703,7 @@ int miclip_encode_text(miclip_model* m, const int64_t* tokens, int32_t P, float*
   if (!m || !tokens || P < 1) return fail(MICLIP_EINVAL, "bad argument to encode_text");
   if (!tower_loaded(m, false))
     return fail(MICLIP_ENOWEIGHTS, "text weights not loaded (missing " + missing(m, false) + ")");
+  if (int rc0 = ensure_folded(m, false)) return rc0;
   hipStream_t s = (hipStream_t)stream;
   const auto& c = m->cfg;
   const int L = c.context_length, W = c.transformer_width, H = c.transformer_heads;
@@ -811,6 +865,29 @@ int miclip_op_gemm(int32_t dtype, const void* A, const void* W, const float* bia
   } else {
     return fail(MICLIP_EINVAL, "unknown epilogue");
   }
+  return 0;
+}
+
+int miclip_op_ln_stats(const void* x, float* stats, int32_t R, int32_t D, void* stream) {
+  if (!x || !stats) return fail(MICLIP_EINVAL, "null argument");
+  MICLIP_HIP(ln_stats(x, stats, R, D, (hipStream_t)stream));
+  return 0;
+}
+
+int miclip_op_ln_fold(int32_t dtype, const void* W, const float* gamma, const float* beta,
+                      const float* bias, void* Wf, float* colsum, float* c, int32_t N, int32_t K,
+                      void* stream) {
+  if (!W || !gamma || !beta || !Wf || !colsum || !c) return fail(MICLIP_EINVAL, "null argument");
+  MICLIP_HIP(ln_fold(dtype, W, gamma, beta, bias, Wf, colsum, c, N, K, (hipStream_t)stream));
+  return 0;
+}
+
+int miclip_op_gemm_ln(int32_t dtype, const void* A, const void* Wf, const float* c,
+                      const float* colsum, const float* stats, void* C, int32_t M, int32_t N,
+                      int32_t K, int32_t act, int32_t variant, void* stream) {
+  if (!A || !Wf || !c || !colsum || !stats || !C) return fail(MICLIP_EINVAL, "null argument");
+  MICLIP_HIP(gemm_store_ln(dtype, A, Wf, c, colsum, stats, C, M, N, K, act, (hipStream_t)stream,
+                           variant));
   return 0;
 }
 

@@ -161,6 +161,69 @@ struct EpiStore {
   }
 };
 
+// LayerNorm folded into the projection that consumes it (ln_1 -> QKV, ln_2 ->
+// c_fc; clip/model.py:184-185). With n = (x - mu) * rs the normalised row,
+//   LN(x) . W^T + b = rs * (x . W'^T - mu * s) + c,
+//   W' = W diag(gamma) (compute dtype), s_j = sum_k W'_jk, c_j = b_j + sum_k beta_k W_jk,
+// so the GEMM reads the fp16 residual stream x directly and the normalised
+// activations h are never written or re-read. Per row {mu, rs} comes from
+// ln_stats (norm.hip: the LayerNorm kernel's own two-pass statistics); s and c
+// are built once per weight load (ln_fold). `bias` holds c. The persistent
+// kernel stages each tile's 256 row statistics in LDS and calls put4ln; the
+// other kernels call put4 / put1, which load them here. Same float expression
+// on every path (pinned by fin), so the tile and tail paths agree bit for bit.
+template <typename T, int ACT>
+struct EpiStoreLN {
+  T* C;
+  const float* bias;     // c
+  const float* colsum;   // s
+  const float2* stats;   // [M] {mu, rs}
+  int ldc;
+  MICLIP_DEV float4 bias4(int col) const { return ld_bias4(bias, col); }
+  MICLIP_DEV float4 bias4nb(int col) const { return ld_bias4_nb(bias, col); }
+  MICLIP_DEV float bias1(int col) const { return bias[col]; }
+  MICLIP_DEV float4 colsum4nb(int col) const { return ld_bias4_nb(colsum, col); }
+  MICLIP_DEV static float fin(float y) {
+    asm volatile("" : "+v"(y));
+    return y;
+  }
+  MICLIP_DEV static float z(float v, float s, float2 st, float c) {
+    return fin(__builtin_fmaf(st.y, __builtin_fmaf(-st.x, s, v), c));
+  }
+  template <bool ASM = false>
+  MICLIP_DEV void put4ln(int r, int c, float4 v, float4 b, float4 s, float2 st) const {
+    const f32x2 y0 = {z(v.x, s.x, st, b.x), z(v.y, s.y, st, b.y)};
+    const f32x2 y1 = {z(v.z, s.z, st, b.z), z(v.w, s.w, st, b.w)};
+    i16x4 o;
+    if constexpr (ACT == ACT_GELU || ACT == ACT_QUICKGELU) {
+      const f32x2 lo = ACT == ACT_GELU ? gelu_erf2(y0) : quick_gelu2(y0);
+      const f32x2 hi = ACT == ACT_GELU ? gelu_erf2(y1) : quick_gelu2(y1);
+      o[0] = to_bits<T>(fin(lo[0]));
+      o[1] = to_bits<T>(fin(lo[1]));
+      o[2] = to_bits<T>(fin(hi[0]));
+      o[3] = to_bits<T>(fin(hi[1]));
+    } else {
+      o[0] = to_bits<T>(y0[0]);
+      o[1] = to_bits<T>(y0[1]);
+      o[2] = to_bits<T>(y1[0]);
+      o[3] = to_bits<T>(y1[1]);
+    }
+    if constexpr (ASM)
+      st_b64_asm(C + (size_t)r * ldc + c, o);
+    else
+      *(i16x4*)(C + (size_t)r * ldc + c) = o;
+  }
+  template <bool ASM = false>
+  MICLIP_DEV void put4(int r, int c, float4 v, float4 b) const {
+    put4ln<ASM>(r, c, v, b, *(const float4*)(colsum + c), stats[r]);
+  }
+  MICLIP_DEV void put1(int r, int c, float v, float b) const {
+    C[(size_t)r * ldc + c] = to_t<T>(fin(act_fn<ACT>(z(v, colsum[c], stats[r], b))));
+  }
+};
+template <class Epi> struct IsLN : std::false_type {};
+template <typename T, int ACT> struct IsLN<EpiStoreLN<T, ACT>> : std::true_type {};
+
 // Residual stream X (R = float, or _Float16 as in the reference's fp16 GPU
 // model, clip/model.py:184-185 `x = x + ...` on half tensors) += acc + bias.
 // fp16: one rounding of x + (acc + bias) (the reference rounds acc + bias

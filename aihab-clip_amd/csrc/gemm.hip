@@ -790,8 +790,12 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
   constexpr int HALF = 128 * 128;        // bytes of one half-tile slot
   constexpr int EPI_LD = 260;            // fp32 row stride of the epilogue staging
   constexpr int STG = 4 * HALF;          // staging: 64 rows in the buffer-1 half onward
-  constexpr int SMEM = 8 * HALF > STG + 64 * EPI_LD * 4 ? 8 * HALF : STG + 64 * EPI_LD * 4;
+  constexpr int SMEM0 = 8 * HALF > STG + 64 * EPI_LD * 4 ? 8 * HALF : STG + 64 * EPI_LD * 4;
+  // folded LayerNorm (EpiStoreLN): the tile's 256 row statistics after the staging
+  constexpr int SMEM = SMEM0 + (IsLN<Epi>::value ? 256 * 8 + 256 * 4 : 0);
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+  float2* lnst = (float2*)(smem + SMEM0);              // [256] {mean, rstd}
+  float4* lncs = (float4*)(smem + SMEM0 + 256 * 8);    // [64] column sums
 
   const int ntn = N / 256, ntm = ntm_dp, ndp = ntm * ntn, nk = K / 64;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -931,6 +935,16 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
     // tile's first MFMA that reuses its registers (draining the prefetch/stores)
     const float4 bv = epi.bias4nb(cn0 + ec);   // branch-free (null bias -> zeros)
     asm volatile("" ::"v"(bv.x), "v"(bv.y), "v"(bv.z), "v"(bv.w));
+    if constexpr (IsLN<Epi>::value) {
+      // the tile's row statistics and column sums, retired here like the bias
+      // and parked in LDS (read after the first pass's barrier)
+      const float4 sv = epi.colsum4nb(cn0 + ec);
+      const int sr = cm0 + (tid & 255);
+      const float2 st = epi.stats[sr < M ? sr : M - 1];
+      asm volatile("" ::"v"(sv.x), "v"(sv.y), "v"(sv.z), "v"(sv.w), "v"(st.x), "v"(st.y));
+      if (tid < 256) lnst[tid] = st;
+      if (tid < 64) lncs[tid] = sv;
+    }
     const int nid = id + gridDim.x;
     if (nid < ndp) {
       sources(nid, m0, n0, asrc, bsrc);
@@ -979,8 +993,22 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
               }
       }
       lds_barrier();
+      if constexpr (IsLN<Epi>::value) {
+        // two rows' worth of LDS reads in flight: the row statistics would
+        // otherwise push the fully unrolled loop past 256 VGPRs (spills)
+        const float4 cs = lncs[tid & 63];
+#pragma unroll 2
+        for (int k = 0; k < 8; ++k) {
+          const int lr = (tid >> 6) + 8 * k;
+          const int row = cm0 + p * 64 + lr;
+          if (full || row < M)
+            epi.put4ln(row, cn0 + ec, *(const float4*)(stg + lr * EPI_LD + ec), bv, cs,
+                       lnst[p * 64 + lr]);
+        }
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
+        if constexpr (IsLN<Epi>::value) break;
         const int lr = (tid >> 6) + 8 * k;
         const int row = cm0 + p * 64 + lr;
         if (full || row < M) {
@@ -1683,6 +1711,32 @@ hipError_t gemm_store(int dtype, const void* A, const void* W, const float* bias
                       int N, int K, int act, hipStream_t s, int v) {
   if (dtype == kF16) return gemm_store_t<_Float16>(A, W, bias, C, M, N, K, act, s, v);
   return gemm_store_t<__bf16>(A, W, bias, C, M, N, K, act, s, v);
+}
+
+template <typename T>
+hipError_t gemm_store_ln_t(const void* A, const void* W, const float* c, const float* colsum,
+                           const void* stats, void* C, int M, int N, int K, int act,
+                           hipStream_t s, int v) {
+  const float2* st = (const float2*)stats;
+  switch (act) {
+    case ACT_NONE:
+      return launch<T>(A, W, M, N, K, EpiStoreLN<T, ACT_NONE>{(T*)C, c, colsum, st, N}, s, v);
+    case ACT_QUICKGELU:
+      return launch<T>(A, W, M, N, K, EpiStoreLN<T, ACT_QUICKGELU>{(T*)C, c, colsum, st, N}, s,
+                       v);
+    case ACT_GELU:
+      return launch<T>(A, W, M, N, K, EpiStoreLN<T, ACT_GELU>{(T*)C, c, colsum, st, N}, s, v);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+hipError_t gemm_store_ln(int dtype, const void* A, const void* W, const float* c,
+                         const float* colsum, const void* stats, void* C, int M, int N, int K,
+                         int act, hipStream_t s, int v) {
+  if (!c || !colsum || !stats) return hipErrorInvalidValue;
+  if (dtype == kF16) return gemm_store_ln_t<_Float16>(A, W, c, colsum, stats, C, M, N, K, act, s, v);
+  return gemm_store_ln_t<__bf16>(A, W, c, colsum, stats, C, M, N, K, act, s, v);
 }
 
 hipError_t gemm_residual(int dtype, const void* A, const void* W, const float* bias, void* X,

@@ -17,6 +17,12 @@ enum Act { ACT_NONE = 0, ACT_QUICKGELU = 1, ACT_GELU = 2 };
 // `variant`: 0 = pick by size, 128 / 256 = force that tile (tests, A/B timing).
 hipError_t gemm_store(int dtype, const void* A, const void* W, const float* bias, void* C,
                       int M, int N, int K, int act, hipStream_t s, int variant = 0);
+// LayerNorm folded into the GEMM (epilogue.h, EpiStoreLN): A = the un-normalised
+// rows, W = W diag(gamma) (ln_fold), stats [M] float2 {mean, rstd} (ln_stats);
+// C = act(rstd * (acc - mean * colsum) + c).
+hipError_t gemm_store_ln(int dtype, const void* A, const void* W, const float* c,
+                         const float* colsum, const void* stats, void* C, int M, int N, int K,
+                         int act, hipStream_t s, int variant = 0);
 // Residual epilogue: X (ld = N) += acc + bias; X fp32, or fp16 when resid16
 // (fp16 compute only: the reference's fp16 GPU residual stream).
 hipError_t gemm_residual(int dtype, const void* A, const void* W, const float* bias, void* X,
@@ -56,6 +62,16 @@ hipError_t layernorm(int dtype, const void* in, const int32_t* rows, int in_stri
                      const float* gamma, const float* beta, float* out_f32, void* out_t,
                      int R, int D, int normalize, hipStream_t s, int in16 = 0,
                      void* out_q = nullptr, void* out_s = nullptr);
+
+// Row statistics of the fp16 residual stream for the folded LayerNorm: stats[r] =
+// {mean, rstd} of row r of in [R, D], exactly as layernorm computes them.
+hipError_t ln_stats(const void* in, float* stats, int R, int D, hipStream_t s);
+// Fold LayerNorm (gamma, beta) into the following Linear (W [N, K] compute dtype,
+// bias [N] fp32 or null): Wf = W diag(gamma) (compute dtype), colsum[j] = sum_k Wf[j,k],
+// c[j] = bias[j] + sum_k beta[k] W[j,k] (sums in double, fixed order).
+hipError_t ln_fold(int dtype, const void* W, const float* gamma, const float* beta,
+                   const float* bias, void* Wf, float* colsum, float* c, int N, int K,
+                   hipStream_t s);
 
 // ---- fused multi-head attention over a packed QKV buffer ----
 // qkv: [B*N, 3*H*dh] compute dtype (torch in_proj order q|k|v); out: [B*N, H*dh].

@@ -185,6 +185,74 @@ __global__ __launch_bounds__(256) void layernorm_h2_kernel(const _Float16* in,  
   }
 }
 
+// Statistics only (folded LayerNorm, epilogue.h EpiStoreLN): the same rows per
+// wave, loads and reductions as layernorm_h2_kernel, so {mean, rstd} are the
+// values that kernel normalises with; one 8-byte store per row.
+template <int NI>
+__global__ __launch_bounds__(256) void ln_stats_kernel(const _Float16* __restrict__ in,
+                                                       float2* __restrict__ stats, int R, int D) {
+  const int lane = threadIdx.x & 63, hl = lane & 31;
+  const int r = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  if ((blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 >= R) return;
+  const bool valid = r < R;
+  const _Float16* src = in + (size_t)(valid ? r : R - 1) * D + hl * 8;
+  float v[NI][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const i16x8 h = *(const i16x8*)(src + i * 256);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[i][e] = from_bits<_Float16>(h[e]);
+    s += ((v[i][0] + v[i][1]) + (v[i][2] + v[i][3])) + ((v[i][4] + v[i][5]) + (v[i][6] + v[i][7]));
+  }
+  const float mean = half_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = v[i][e] - mean;
+      q += d * d;
+    }
+  const float rstd = rsqrtf(half_sum(q) / (float)D + 1e-5f);
+  if (valid && hl == 0) stats[r] = make_float2(mean, rstd);
+}
+
+// One workgroup per output row j: Wf[j,:] = W[j,:] * gamma, colsum[j] = sum Wf[j,:],
+// c[j] = bias[j] + beta . W[j,:]; per-thread double partials, fixed-order LDS tree.
+template <typename T>
+__global__ __launch_bounds__(256) void ln_fold_kernel(const T* __restrict__ W,
+                                                      const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta,
+                                                      const float* __restrict__ bias,
+                                                      T* __restrict__ Wf, float* __restrict__ colsum,
+                                                      float* __restrict__ c, int K) {
+  __shared__ double red[2][256];
+  const int j = blockIdx.x, t = threadIdx.x;
+  double ps = 0.0, pc = 0.0;
+  for (int k = t; k < K; k += 256) {
+    const float w = (float)W[(size_t)j * K + k];
+    const T wf = (T)(w * gamma[k]);
+    Wf[(size_t)j * K + k] = wf;
+    ps += (double)(float)wf;
+    pc += (double)beta[k] * (double)w;
+  }
+  red[0][t] = ps;
+  red[1][t] = pc;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (t < h) {
+      red[0][t] += red[0][t + h];
+      red[1][t] += red[1][t + h];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    colsum[j] = (float)red[0][0];
+    c[j] = (float)(red[1][0] + (bias ? (double)bias[j] : 0.0));
+  }
+}
+
 template <typename T, bool MX = false>
 hipError_t ln_h2_dispatch(const _Float16* in, const float* g, const float* b, void* out, int R,
                           int D, hipStream_t s, void* oq = nullptr, void* os = nullptr) {
@@ -233,6 +301,41 @@ hipError_t ln_dispatch(const TI* in, const int32_t* rows, int stride, const floa
 }
 
 }  // namespace
+
+hipError_t ln_stats(const void* in, float* stats, int R, int D, hipStream_t s) {
+  if (R < 1 || D % 256 || D > 1536 || !in || !stats) return hipErrorInvalidValue;
+  const dim3 grid((R + 7) / 8), block(256);
+#define MICLIP_LNS_CASE(V)                                                              \
+  case V:                                                                               \
+    hipLaunchKernelGGL((ln_stats_kernel<V>), grid, block, 0, s, (const _Float16*)in,    \
+                       (float2*)stats, R, D);                                           \
+    break;
+  switch (D / 256) {
+    MICLIP_LNS_CASE(1)
+    MICLIP_LNS_CASE(2)
+    MICLIP_LNS_CASE(3)
+    MICLIP_LNS_CASE(4)
+    MICLIP_LNS_CASE(5)
+    MICLIP_LNS_CASE(6)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef MICLIP_LNS_CASE
+  return hipGetLastError();
+}
+
+hipError_t ln_fold(int dtype, const void* W, const float* gamma, const float* beta,
+                   const float* bias, void* Wf, float* colsum, float* c, int N, int K,
+                   hipStream_t s) {
+  if (N < 1 || K < 1 || !W || !gamma || !beta || !Wf || !colsum || !c) return hipErrorInvalidValue;
+  if (dtype == kF16)
+    hipLaunchKernelGGL((ln_fold_kernel<_Float16>), dim3(N), dim3(256), 0, s, (const _Float16*)W,
+                       gamma, beta, bias, (_Float16*)Wf, colsum, c, K);
+  else
+    hipLaunchKernelGGL((ln_fold_kernel<__bf16>), dim3(N), dim3(256), 0, s, (const __bf16*)W,
+                       gamma, beta, bias, (__bf16*)Wf, colsum, c, K);
+  return hipGetLastError();
+}
 
 hipError_t layernorm(int dtype, const void* in, const int32_t* rows, int in_stride_rows,
                      const float* gamma, const float* beta, float* out_f32, void* out_t, int R,

@@ -24,7 +24,8 @@ EXPORTS = (
     "miclip_encode_image", "miclip_encode_text", "miclip_zero_shot",
     "miclip_model_destroy", "miclip_last_error", "miclip_abi_version",
     "miclip_model_bytes", "miclip_set_profiling", "miclip_profile_read", "miclip_set_splits",
-    "miclip_op_gemm", "miclip_op_layernorm", "miclip_op_attention", "miclip_preprocess",
+    "miclip_op_gemm", "miclip_op_ln_stats", "miclip_op_ln_fold", "miclip_op_gemm_ln",
+    "miclip_op_layernorm", "miclip_op_attention", "miclip_preprocess",
     "miclip_row_norms", "miclip_class_centroids", "miclip_proto_scores",
     "miclip_mx_scale_bytes", "miclip_op_quant_mx", "miclip_op_gemm_mx", "miclip_op_layernorm_mx",
 )
@@ -89,6 +90,10 @@ def load_library(path: str = None):
         "miclip_profile_read": ([vp, ctypes.POINTER(MiclipKernelStat), i32, i32], ctypes.c_int),
         "miclip_op_gemm": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp], ctypes.c_int),
         "miclip_op_layernorm": ([i32, vp, vp, vp, vp, i32, i32, i32, vp], ctypes.c_int),
+        "miclip_op_ln_stats": ([vp, vp, i32, i32, vp], ctypes.c_int),
+        "miclip_op_ln_fold": ([i32, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp], ctypes.c_int),
+        "miclip_op_gemm_ln": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
+                              ctypes.c_int),
         "miclip_op_attention": ([i32, vp, vp, i32, i32, i32, i32, i32, i32, vp], ctypes.c_int),
         "miclip_mx_scale_bytes": ([i32, i32], i64),
         "miclip_op_quant_mx": ([vp, i32, i32, i32, vp, vp, vp], ctypes.c_int),

@@ -211,6 +211,21 @@ int miclip_op_gemm(int32_t dtype, const void* A, const void* W, const float* bia
                    int32_t M, int32_t N, int32_t K, int32_t epi, int32_t act, int32_t variant,
                    void* stream);
 
+/* Folded LayerNorm (ln_1 -> QKV, ln_2 -> c_fc of ResidualAttentionBlock,
+ * clip/model.py:184-185): LN(x) . W^T + b computed as rstd * (x . Wf^T - mean * colsum) + c.
+ * miclip_op_ln_stats: stats[r] = {mean, rstd} (fp32 pairs) of the fp16 rows x [R, D].
+ * miclip_op_ln_fold: Wf = W diag(gamma) (dtype), colsum = row sums of Wf, c = bias + W beta
+ *   (W [N, K] dtype; gamma, beta [K], bias [N] fp32, bias may be null).
+ * miclip_op_gemm_ln: C [M, N] (dtype) = act(rstd * (A . Wf^T - mean * colsum) + c), A [M, K]
+ *   the un-normalised rows (act as miclip_op_gemm; variant as there). */
+int miclip_op_ln_stats(const void* x, float* stats, int32_t R, int32_t D, void* stream);
+int miclip_op_ln_fold(int32_t dtype, const void* W, const float* gamma, const float* beta,
+                      const float* bias, void* Wf, float* colsum, float* c, int32_t N, int32_t K,
+                      void* stream);
+int miclip_op_gemm_ln(int32_t dtype, const void* A, const void* Wf, const float* c,
+                      const float* colsum, const float* stats, void* C, int32_t M, int32_t N,
+                      int32_t K, int32_t act, int32_t variant, void* stream);
+
 /* LayerNorm over R rows of width D (eps 1e-5, fp32 statistics); replaces the
  * reference LayerNorm (clip/model.py:151-157). flags bit 0: out fp32 (else compute
  * dtype); bit 1: in fp16 (the fp16 residual stream; dtype MICLIP_FP16 only), else fp32. */
