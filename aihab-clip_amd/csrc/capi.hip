@@ -82,6 +82,7 @@ struct Block {
   // column sums and folded biases (epilogue.h EpiStoreLN)
   void *wf_qkv = nullptr, *wf_fc = nullptr;
   float *cs_qkv = nullptr, *c_qkv = nullptr, *cs_fc = nullptr, *c_fc = nullptr;
+  float *fs_qkv = nullptr, *fs_fc = nullptr;   // [2] each: 1/S of the fold (ln_stats rscale)
 };
 
 struct Workspace {
@@ -275,7 +276,8 @@ int ensure_ws(miclip_model* m, Workspace& w, int items, int ntok, int W, bool im
     if ((rc = dev_alloc(m, &w.patches, (size_t)items * g * g * m->Kp * e))) return rc;
   }
   if ((rc = dev_alloc(m, &w.x, (size_t)rows * W * (m->resid16 ? 2 : 4)))) return rc;
-  if ((rc = dev_alloc(m, &w.h, (size_t)rows * W * e))) return rc;
+  // h (the LayerNorm output) is unused when ln_1 / ln_2 are folded into the GEMMs
+  if (!m->lnfold && (rc = dev_alloc(m, &w.h, (size_t)rows * W * e))) return rc;
   if ((rc = dev_alloc(m, &w.qkv, (size_t)rows * 3 * W * e))) return rc;
   if ((rc = dev_alloc(m, &w.o, (size_t)rows * W * e))) return rc;
   if ((rc = dev_alloc(m, &w.f, (size_t)rows * 4 * W * e))) return rc;
@@ -315,11 +317,13 @@ int ensure_folded(miclip_model* m, bool visual) {
       if ((rc = dev_alloc(m, (void**)&b.c_qkv, (size_t)3 * W * 4))) return rc;
       if ((rc = dev_alloc(m, (void**)&b.cs_fc, (size_t)4 * W * 4))) return rc;
       if ((rc = dev_alloc(m, (void**)&b.c_fc, (size_t)4 * W * 4))) return rc;
+      if ((rc = dev_alloc(m, (void**)&b.fs_qkv, 8))) return rc;
+      if ((rc = dev_alloc(m, (void**)&b.fs_fc, 8))) return rc;
     }
     MICLIP_HIP(ln_fold(m->dtype, b.w_qkv, b.ln1_g, b.ln1_b, b.b_qkv, b.wf_qkv, b.cs_qkv, b.c_qkv,
-                       3 * W, W, nullptr));
+                       3 * W, W, nullptr, b.fs_qkv));
     MICLIP_HIP(ln_fold(m->dtype, b.w_fc, b.ln2_g, b.ln2_b, b.b_fc, b.wf_fc, b.cs_fc, b.c_fc,
-                       4 * W, W, nullptr));
+                       4 * W, W, nullptr, b.fs_fc));
   }
   MICLIP_HIP(hipDeviceSynchronize());
   m->folded[visual ? 0 : 1] = true;
@@ -334,7 +338,7 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
   const bool fold = m->lnfold && b.wf_qkv;
   if (fold) {
     ProfScope p(m, K_LAYERNORM, s, 0, dM * (dW * rb + 8));
-    MICLIP_HIP(ln_stats(w.x, w.stats, M, W, s));
+    MICLIP_HIP(ln_stats(w.x, w.stats, M, W, s, b.fs_qkv));
   } else {
     ProfScope p(m, K_LAYERNORM, s, 0, dM * dW * (rb + (mx ? 1 : 2)));
     if (mx)
@@ -366,7 +370,7 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
   }
   if (fold) {
     ProfScope p(m, K_LAYERNORM, s, 0, dM * (dW * rb + 8));
-    MICLIP_HIP(ln_stats(w.x, w.stats, M, W, s));
+    MICLIP_HIP(ln_stats(w.x, w.stats, M, W, s, b.fs_fc));
   } else {
     ProfScope p(m, K_LAYERNORM, s, 0, dM * dW * (rb + (mx ? 1 : 2)));
     if (mx)
@@ -409,7 +413,7 @@ Workspace view(const miclip_model* m, const Workspace& w, size_t row0, size_t it
   const int g = m->cfg.image_resolution / m->cfg.vision_patch_size;
   if (w.patches) v.patches = (char*)w.patches + item0 * g * g * m->Kp * e;
   v.x = (char*)w.x + row0 * W * (m->resid16 ? 2 : 4);
-  v.h = (char*)w.h + row0 * W * e;
+  if (w.h) v.h = (char*)w.h + row0 * W * e;
   v.qkv = (char*)w.qkv + row0 * 3 * W * e;
   v.o = (char*)w.o + row0 * W * e;
   v.f = (char*)w.f + row0 * 4 * W * e;
@@ -868,17 +872,19 @@ int miclip_op_gemm(int32_t dtype, const void* A, const void* W, const float* bia
   return 0;
 }
 
-int miclip_op_ln_stats(const void* x, float* stats, int32_t R, int32_t D, void* stream) {
+int miclip_op_ln_stats(const void* x, float* stats, int32_t R, int32_t D, const float* rscale,
+                       void* stream) {
   if (!x || !stats) return fail(MICLIP_EINVAL, "null argument");
-  MICLIP_HIP(ln_stats(x, stats, R, D, (hipStream_t)stream));
+  MICLIP_HIP(ln_stats(x, stats, R, D, (hipStream_t)stream, rscale));
   return 0;
 }
 
 int miclip_op_ln_fold(int32_t dtype, const void* W, const float* gamma, const float* beta,
                       const float* bias, void* Wf, float* colsum, float* c, int32_t N, int32_t K,
-                      void* stream) {
+                      float* inv_scale, void* stream) {
   if (!W || !gamma || !beta || !Wf || !colsum || !c) return fail(MICLIP_EINVAL, "null argument");
-  MICLIP_HIP(ln_fold(dtype, W, gamma, beta, bias, Wf, colsum, c, N, K, (hipStream_t)stream));
+  MICLIP_HIP(ln_fold(dtype, W, gamma, beta, bias, Wf, colsum, c, N, K, (hipStream_t)stream,
+                     inv_scale));
   return 0;
 }
 

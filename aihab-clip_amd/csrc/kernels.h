@@ -64,14 +64,18 @@ hipError_t layernorm(int dtype, const void* in, const int32_t* rows, int in_stri
                      void* out_q = nullptr, void* out_s = nullptr);
 
 // Row statistics of the fp16 residual stream for the folded LayerNorm: stats[r] =
-// {mean, rstd} of row r of in [R, D], exactly as layernorm computes them.
-hipError_t ln_stats(const void* in, float* stats, int R, int D, hipStream_t s);
+// {mean, rstd * *rscale} of row r of in [R, D], mean and rstd exactly as layernorm
+// computes them; rscale (device, nullable = 1) is the weight's 1/S from ln_fold.
+hipError_t ln_stats(const void* in, float* stats, int R, int D, hipStream_t s,
+                    const float* rscale = nullptr);
 // Fold LayerNorm (gamma, beta) into the following Linear (W [N, K] compute dtype,
-// bias [N] fp32 or null): Wf = W diag(gamma) (compute dtype), colsum[j] = sum_k Wf[j,k],
-// c[j] = bias[j] + sum_k beta[k] W[j,k] (sums in double, fixed order).
+// bias [N] fp32 or null): Wf = W diag(gamma) * S (compute dtype), colsum[j] = sum_k Wf[j,k],
+// c[j] = bias[j] + sum_k beta[k] W[j,k] (sums in double, fixed order). S is the power
+// of two that puts max|W gamma| S in [2^14, 2^15] (no fp16 subnormals for small
+// gamma); inv_scale (device float[2], nullable = no scaling) receives 1/S in [0].
 hipError_t ln_fold(int dtype, const void* W, const float* gamma, const float* beta,
                    const float* bias, void* Wf, float* colsum, float* c, int N, int K,
-                   hipStream_t s);
+                   hipStream_t s, float* inv_scale = nullptr);
 
 // ---- fused multi-head attention over a packed QKV buffer ----
 // qkv: [B*N, 3*H*dh] compute dtype (torch in_proj order q|k|v); out: [B*N, H*dh].

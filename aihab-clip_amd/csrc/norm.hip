@@ -188,9 +188,12 @@ __global__ __launch_bounds__(256) void layernorm_h2_kernel(const _Float16* in,  
 // Statistics only (folded LayerNorm, epilogue.h EpiStoreLN): the same rows per
 // wave, loads and reductions as layernorm_h2_kernel, so {mean, rstd} are the
 // values that kernel normalises with; one 8-byte store per row.
+// rscale (nullable): the folded weight's 1/S (ln_fold), a power of two, so
+// {mean, rstd / S} is exact and the GEMM epilogue needs no extra multiply.
 template <int NI>
 __global__ __launch_bounds__(256) void ln_stats_kernel(const _Float16* __restrict__ in,
-                                                       float2* __restrict__ stats, int R, int D) {
+                                                       float2* __restrict__ stats, int R, int D,
+                                                       const float* __restrict__ rscale) {
   const int lane = threadIdx.x & 63, hl = lane & 31;
   const int r = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
   if ((blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 >= R) return;
@@ -215,24 +218,56 @@ __global__ __launch_bounds__(256) void ln_stats_kernel(const _Float16* __restric
       q += d * d;
     }
   const float rstd = rsqrtf(half_sum(q) / (float)D + 1e-5f);
-  if (valid && hl == 0) stats[r] = make_float2(mean, rstd);
+  if (valid && hl == 0) stats[r] = make_float2(mean, rscale ? rstd * *rscale : rstd);
 }
 
-// One workgroup per output row j: Wf[j,:] = W[j,:] * gamma, colsum[j] = sum Wf[j,:],
+// max |W[j,k] * gamma[k]| over the matrix, as the bits of a non-negative float
+// (ordered like unsigned ints) in *amax, which the caller zeroes.
+template <typename T>
+__global__ __launch_bounds__(256) void fold_amax_kernel(const T* __restrict__ W,
+                                                        const float* __restrict__ gamma,
+                                                        unsigned* __restrict__ amax, int N, int K) {
+  float m = 0.f;
+  const size_t n = (size_t)N * K;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    m = fmaxf(m, fabsf((float)W[i] * gamma[i % K]));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(m));
+}
+
+// S = 2^(15 - E) for amax = f * 2^E, f in [0.5, 1): the largest folded weight
+// lands in [2^14, 2^15], well inside fp16's range, so small gamma never pushes
+// W * gamma into the fp16 subnormals (the reference applies gamma in fp32,
+// clip/model.py:154-157). Exact power of two: dividing it back out is exact.
+MICLIP_DEV float fold_scale(unsigned amax_bits) {
+  const float a = __uint_as_float(amax_bits);
+  if (!(a > 0.f) || !(a < 3.0e38f)) return 1.f;
+  int e;
+  (void)frexpf(a, &e);
+  e = e < -100 ? -100 : (e > 100 ? 100 : e);
+  return ldexpf(1.f, 15 - e);
+}
+
+// One workgroup per output row j: Wf[j,:] = W[j,:] * gamma * S, colsum[j] = sum Wf[j,:],
 // c[j] = bias[j] + beta . W[j,:]; per-thread double partials, fixed-order LDS tree.
+// Block 0 also stores 1/S (the ln_stats rscale of this weight) when inv_scale is set.
 template <typename T>
 __global__ __launch_bounds__(256) void ln_fold_kernel(const T* __restrict__ W,
                                                       const float* __restrict__ gamma,
                                                       const float* __restrict__ beta,
                                                       const float* __restrict__ bias,
                                                       T* __restrict__ Wf, float* __restrict__ colsum,
-                                                      float* __restrict__ c, int K) {
+                                                      float* __restrict__ c, int K,
+                                                      const unsigned* __restrict__ amax,
+                                                      float* __restrict__ inv_scale) {
   __shared__ double red[2][256];
   const int j = blockIdx.x, t = threadIdx.x;
+  const float S = amax ? fold_scale(*amax) : 1.f;
+  if (inv_scale && j == 0 && t == 0) *inv_scale = 1.f / S;
   double ps = 0.0, pc = 0.0;
   for (int k = t; k < K; k += 256) {
     const float w = (float)W[(size_t)j * K + k];
-    const T wf = (T)(w * gamma[k]);
+    const T wf = (T)((w * gamma[k]) * S);
     Wf[(size_t)j * K + k] = wf;
     ps += (double)(float)wf;
     pc += (double)beta[k] * (double)w;
@@ -302,13 +337,14 @@ hipError_t ln_dispatch(const TI* in, const int32_t* rows, int stride, const floa
 
 }  // namespace
 
-hipError_t ln_stats(const void* in, float* stats, int R, int D, hipStream_t s) {
+hipError_t ln_stats(const void* in, float* stats, int R, int D, hipStream_t s,
+                    const float* rscale) {
   if (R < 1 || D % 256 || D > 1536 || !in || !stats) return hipErrorInvalidValue;
   const dim3 grid((R + 7) / 8), block(256);
 #define MICLIP_LNS_CASE(V)                                                              \
   case V:                                                                               \
     hipLaunchKernelGGL((ln_stats_kernel<V>), grid, block, 0, s, (const _Float16*)in,    \
-                       (float2*)stats, R, D);                                           \
+                       (float2*)stats, R, D, rscale);                                   \
     break;
   switch (D / 256) {
     MICLIP_LNS_CASE(1)
@@ -326,14 +362,28 @@ hipError_t ln_stats(const void* in, float* stats, int R, int D, hipStream_t s) {
 
 hipError_t ln_fold(int dtype, const void* W, const float* gamma, const float* beta,
                    const float* bias, void* Wf, float* colsum, float* c, int N, int K,
-                   hipStream_t s) {
+                   hipStream_t s, float* inv_scale) {
   if (N < 1 || K < 1 || !W || !gamma || !beta || !Wf || !colsum || !c) return hipErrorInvalidValue;
+  // inv_scale is a device float[2]: [0] receives 1/S, [1] is the amax scratch word
+  unsigned* amax = inv_scale ? (unsigned*)(inv_scale + 1) : nullptr;
+  if (amax) {
+    hipError_t e = hipMemsetAsync(amax, 0, sizeof(unsigned), s);
+    if (e != hipSuccess) return e;
+    const size_t want = ((size_t)N * K + 4095) / 4096;   // >= 16 elements per thread
+    const int blocks = (int)(want < 1024 ? want : 1024);
+    if (dtype == kF16)
+      hipLaunchKernelGGL((fold_amax_kernel<_Float16>), dim3(blocks), dim3(256), 0, s,
+                         (const _Float16*)W, gamma, amax, N, K);
+    else
+      hipLaunchKernelGGL((fold_amax_kernel<__bf16>), dim3(blocks), dim3(256), 0, s,
+                         (const __bf16*)W, gamma, amax, N, K);
+  }
   if (dtype == kF16)
     hipLaunchKernelGGL((ln_fold_kernel<_Float16>), dim3(N), dim3(256), 0, s, (const _Float16*)W,
-                       gamma, beta, bias, (_Float16*)Wf, colsum, c, K);
+                       gamma, beta, bias, (_Float16*)Wf, colsum, c, K, amax, inv_scale);
   else
     hipLaunchKernelGGL((ln_fold_kernel<__bf16>), dim3(N), dim3(256), 0, s, (const __bf16*)W,
-                       gamma, beta, bias, (__bf16*)Wf, colsum, c, K);
+                       gamma, beta, bias, (__bf16*)Wf, colsum, c, K, amax, inv_scale);
   return hipGetLastError();
 }
 

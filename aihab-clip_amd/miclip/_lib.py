@@ -10,7 +10,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MICLIP_LIB", os.path.join(_HERE, "libmiclip.so"))
 
-ABI_VERSION = 3          # include/miclip.h MICLIP_ABI_VERSION
+ABI_VERSION = 4          # include/miclip.h MICLIP_ABI_VERSION
 MICLIP_FP16 = 0
 MICLIP_BF16 = 1
 MICLIP_MXFP8 = 2
@@ -90,8 +90,8 @@ def load_library(path: str = None):
         "miclip_profile_read": ([vp, ctypes.POINTER(MiclipKernelStat), i32, i32], ctypes.c_int),
         "miclip_op_gemm": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp], ctypes.c_int),
         "miclip_op_layernorm": ([i32, vp, vp, vp, vp, i32, i32, i32, vp], ctypes.c_int),
-        "miclip_op_ln_stats": ([vp, vp, i32, i32, vp], ctypes.c_int),
-        "miclip_op_ln_fold": ([i32, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp], ctypes.c_int),
+        "miclip_op_ln_stats": ([vp, vp, i32, i32, vp, vp], ctypes.c_int),
+        "miclip_op_ln_fold": ([i32, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, vp], ctypes.c_int),
         "miclip_op_gemm_ln": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
                               ctypes.c_int),
         "miclip_op_attention": ([i32, vp, vp, i32, i32, i32, i32, i32, i32, vp], ctypes.c_int),

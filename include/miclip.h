@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MICLIP_ABI_VERSION 3
+#define MICLIP_ABI_VERSION 4
 
 enum miclip_status {
   MICLIP_OK = 0,
@@ -212,16 +212,22 @@ int miclip_op_gemm(int32_t dtype, const void* A, const void* W, const float* bia
                    void* stream);
 
 /* Folded LayerNorm (ln_1 -> QKV, ln_2 -> c_fc of ResidualAttentionBlock,
- * clip/model.py:184-185): LN(x) . W^T + b computed as rstd * (x . Wf^T - mean * colsum) + c.
- * miclip_op_ln_stats: stats[r] = {mean, rstd} (fp32 pairs) of the fp16 rows x [R, D].
- * miclip_op_ln_fold: Wf = W diag(gamma) (dtype), colsum = row sums of Wf, c = bias + W beta
- *   (W [N, K] dtype; gamma, beta [K], bias [N] fp32, bias may be null).
- * miclip_op_gemm_ln: C [M, N] (dtype) = act(rstd * (A . Wf^T - mean * colsum) + c), A [M, K]
+ * clip/model.py:184-185): LN(x) . W^T + b computed as rs * (x . Wf^T - mean * colsum) + c
+ * with rs = rstd / S.
+ * miclip_op_ln_fold: Wf = W diag(gamma) * S (dtype), colsum = row sums of Wf, c = bias + W beta
+ *   (W [N, K] dtype; gamma, beta [K], bias [N] fp32, bias may be null). S is the power of
+ *   two that puts max|W gamma| S in [2^14, 2^15], so a small gamma never rounds W gamma into
+ *   the fp16 subnormals; inv_scale: device float[2] ([0] receives 1/S, [1] is scratch), or
+ *   NULL for S = 1.
+ * miclip_op_ln_stats: stats[r] = {mean, rstd * *rscale} (fp32 pairs) of the fp16 rows
+ *   x [R, D]; rscale = the fold's inv_scale (device), or NULL for 1.
+ * miclip_op_gemm_ln: C [M, N] (dtype) = act(rs * (A . Wf^T - mean * colsum) + c), A [M, K]
  *   the un-normalised rows (act as miclip_op_gemm; variant as there). */
-int miclip_op_ln_stats(const void* x, float* stats, int32_t R, int32_t D, void* stream);
+int miclip_op_ln_stats(const void* x, float* stats, int32_t R, int32_t D, const float* rscale,
+                       void* stream);
 int miclip_op_ln_fold(int32_t dtype, const void* W, const float* gamma, const float* beta,
                       const float* bias, void* Wf, float* colsum, float* c, int32_t N, int32_t K,
-                      void* stream);
+                      float* inv_scale, void* stream);
 int miclip_op_gemm_ln(int32_t dtype, const void* A, const void* Wf, const float* c,
                       const float* colsum, const float* stats, void* C, int32_t M, int32_t N,
                       int32_t K, int32_t act, int32_t variant, void* stream);
