@@ -849,6 +849,12 @@ void miclip_model_destroy(miclip_model* m) {
 
 int64_t miclip_model_bytes(const miclip_model* m) { return m ? m->bytes : 0; }
 
+int miclip_model_flags(const miclip_model* m) {
+  if (!m) return 0;
+  return (m->resid16 ? MICLIP_MODEL_RESID16 : 0) | (m->lnfold ? MICLIP_MODEL_LNFOLD : 0) |
+         (m->mx ? MICLIP_MODEL_MXFP8 : 0);
+}
+
 int miclip_op_gemm(int32_t dtype, const void* A, const void* W, const float* bias, void* C,
                    int32_t M, int32_t N, int32_t K, int32_t epi, int32_t act, int32_t variant,
                    void* stream) {

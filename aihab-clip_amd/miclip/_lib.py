@@ -18,12 +18,15 @@ MICLIP_ACT_QUICKGELU = 1
 MICLIP_ACT_GELU = 2
 MICLIP_FLAG_NORMALIZE = 1
 MICLIP_FLAG_APPLY_PROJ = 2
+MICLIP_MODEL_RESID16 = 1
+MICLIP_MODEL_LNFOLD = 2
+MICLIP_MODEL_MXFP8 = 4
 
 EXPORTS = (
     "miclip_model_create", "miclip_model_load_weights", "miclip_reserve",
     "miclip_encode_image", "miclip_encode_text", "miclip_zero_shot",
     "miclip_model_destroy", "miclip_last_error", "miclip_abi_version",
-    "miclip_model_bytes", "miclip_set_profiling", "miclip_profile_read", "miclip_set_splits",
+    "miclip_model_bytes", "miclip_model_flags", "miclip_set_profiling", "miclip_profile_read", "miclip_set_splits",
     "miclip_op_gemm", "miclip_op_ln_stats", "miclip_op_ln_fold", "miclip_op_gemm_ln",
     "miclip_op_layernorm", "miclip_op_attention", "miclip_preprocess",
     "miclip_row_norms", "miclip_class_centroids", "miclip_proto_scores",
@@ -85,6 +88,7 @@ def load_library(path: str = None):
         "miclip_last_error": ([], ctypes.c_char_p),
         "miclip_abi_version": ([], ctypes.c_int),
         "miclip_model_bytes": ([vp], i64),
+        "miclip_model_flags": ([vp], ctypes.c_int),
         "miclip_set_profiling": ([vp, ctypes.c_int], ctypes.c_int),
         "miclip_set_splits": ([vp, i32], ctypes.c_int),
         "miclip_profile_read": ([vp, ctypes.POINTER(MiclipKernelStat), i32, i32], ctypes.c_int),

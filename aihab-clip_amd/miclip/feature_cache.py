@@ -289,14 +289,20 @@ def shard_range(n: int, rank: int, world: int):
 
 
 @torch.no_grad()
-def sharded_encode(encode_fn, images: torch.Tensor, group=None, dim: Optional[int] = None):
+def sharded_encode(encode_fn, images, group=None, dim: Optional[int] = None):
     """Encode this rank's contiguous slice of `images` and all-gather the rows.
 
-    `images` is the full batch (every rank sees the same tensor, e.g. from a
+    `images` is the full batch (every rank sees the same batch, e.g. from a
     deterministic loader) -- only rows shard_range(n, rank, world) are encoded
     here. Shards are padded to equal length for all_gather_into_tensor and the
-    result is trimmed back, so the output equals encode_fn(images) row for row.
-    Without an initialised process group it degrades to encode_fn(images).
+    result is trimmed back, so the output equals encode_fn(images) row for row
+    (the row order aihab_utils/feature_cache.py:144-162 relies on).
+
+    The collective's buffers live where the backend needs them, whatever device
+    the loader's images are on: nccl (RCCL) -> this rank's current HIP device,
+    gloo -> host. A rank whose shard is empty (n < world) still joins the
+    gather; it needs `dim`. Without an initialised process group this is
+    encode_fn(images).
     """
     if not (dist.is_available() and dist.is_initialized()):
         return encode_fn(images)
@@ -308,22 +314,24 @@ def sharded_encode(encode_fn, images: torch.Tensor, group=None, dim: Optional[in
     width = dim if dim is not None else (local.shape[1] if local is not None else None)
     if width is None:
         raise ValueError("sharded_encode needs `dim` when a rank has an empty shard")
-    per = -(-n // world)
-    if local is not None:
-        dev = local.device
-    elif isinstance(images, torch.Tensor):
-        dev = images.device
+    if dist.get_backend(group) == "nccl":
+        dev = torch.device("cuda", torch.cuda.current_device())
     else:
-        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
-            else torch.device("cpu")
-    buf = torch.zeros(per, width, device=dev, dtype=torch.float32)
-    if local is not None:
-        buf[: hi - lo] = local
+        dev = torch.device("cpu")
+    per = -(-n // world)
+    if (local is not None and hi - lo == per and local.device == dev
+            and local.dtype == torch.float32 and local.is_contiguous()):
+        buf = local
+    else:
+        buf = torch.zeros(per, width, device=dev, dtype=torch.float32)
+        if local is not None:
+            buf[: hi - lo] = local
     out = torch.empty(world * per, width, device=dev, dtype=torch.float32)
     dist.all_gather_into_tensor(out, buf, group=group)
-    keep = torch.cat([out[r * per: r * per + (shard_range(n, r, world)[1] - shard_range(n, r, world)[0])]
-                      for r in range(world)])
-    return keep
+    if n != world * per:
+        out = torch.cat([out[r * per: r * per + (shard_range(n, r, world)[1] - shard_range(n, r, world)[0])]
+                         for r in range(world)])
+    return out if local is None else out.to(local.device)
 
 
 @torch.no_grad()

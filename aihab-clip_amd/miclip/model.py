@@ -169,6 +169,14 @@ class CLIP(nn.Module):
         h = self._require()
         _lib.check(h.lib.miclip_set_splits(h.ptr, int(splits)), "miclip_set_splits")
 
+    def numerics(self):
+        """The handle's numerics path: dict(resid16, lnfold, mxfp8) (miclip_model_flags)."""
+        h = self._require()
+        f = h.lib.miclip_model_flags(h.ptr)
+        return dict(resid16=bool(f & _lib.MICLIP_MODEL_RESID16),
+                    lnfold=bool(f & _lib.MICLIP_MODEL_LNFOLD),
+                    mxfp8=bool(f & _lib.MICLIP_MODEL_MXFP8))
+
     def set_profiling(self, enable=True):
         h = self._require()
         _lib.check(h.lib.miclip_set_profiling(h.ptr, int(bool(enable))), "miclip_set_profiling")

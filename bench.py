@@ -2,26 +2,39 @@
 """Benchmark: images/sec of the CLIP feature-cache encode on MI355X.
 
 One step = the hot path of the reference's feature-cache loop
-(aihab_utils/feature_cache.py:114-142 / methods/utils.py:142-173) on one
-device-resident batch per GPU:
-    encode_image (ViT, all HIP kernels) -> L2-normalise (fused into ln_post)
-    -> RCCL all-gather of the normalised embeddings over the ranks (N > 1)
+(aihab_utils/feature_cache.py:114-142 / methods/utils.py:142-173) over one
+device-resident global batch, through the product's sharded driver
+(miclip.feature_cache.sharded_encode):
+    each rank encodes its contiguous slice (encode_image, all HIP kernels,
+    L2-normalise fused into ln_post)
+    -> RCCL all-gather of the normalised embeddings back into the global row
+       order (N > 1; aihab_utils/feature_cache.py:144-162)
     -> zero-shot logits of the gathered rows (x @ visual.proj -> normalise
        -> 100 * f @ text_weights -> top-1; methods/ProLIP.py:288-293).
-Per-GPU batch is fixed (weak scaling); `value` = all ranks' images / max-over-
-ranks wall time of the K timed steps.
+--scaling weak (default): 256 images per GPU, global batch 256 N.
+--scaling strong: global batch 256 split 256/N per GPU.
+`value` = global images per step * K / max-over-ranks wall time of the K steps.
 
-Also reported (rank 0): the dominant kernel's roofline (MLP c_fc GEMM,
+`python bench.py --gpus N` starts the N ranks itself (one process per GPU,
+spawned before anything touches the GPU); under torchrun (WORLD_SIZE set) it
+is one of the ranks. n_gpus is the world size RCCL actually formed.
+
+Also reported (rank 0): the dominant kernel's roofline (MLP c_fc GEMM:
 algorithmic FLOPs / its average launch time from HIP events of one profiled
-step), the whole-path MFMA fraction, and the reference CPU encode (the
-repo's fp32 torch-CPU restatement of clip/model.py, oracle/clip_oracle.py,
-bit-exact with the reference) timed on this host on a bounded sample.
+step, which runs the batch unsplit on one stream; traffic from the committed
+PMC profile of that same kernel and launch shape, else null), the whole-path
+MFMA fraction, and the reference CPU encode (the repo's fp32 torch-CPU
+restatement of clip/model.py, oracle/clip_oracle.py, bit-exact with the
+reference on the same machine) timed on this host on a bounded sample.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--model ViT-L/14] [--batch 256]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling weak|strong]
+                    [--model ViT-L/14] [--batch 256] [--ab-splits] [--ab-fold]
 """
 import argparse
 import json
 import os
+import socket
+import statistics
 import sys
 import time
 
@@ -30,21 +43,73 @@ for _p in (os.path.join(ROOT, "aihab-clip_amd"), ROOT):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
 METRIC = "images/sec encoded (ViT-L/14 bs=256) at 1/2/4/8 GPUs; % bf16 MFMA roofline"
 PEAK_TFLOPS = 256 * 2.4e9 * 4096 / 1e12   # dense bf16/fp16 MFMA, MI355X_MICROARCH.md
-PEAK_HBM_GBS = 8000.0
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "traffic_gemm_fc.json")
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--model", default="ViT-L/14")
+    ap.add_argument("--batch", type=int, default=256,
+                    help="images per GPU (weak) or global images (strong) per step")
+    ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16", "mxfp8"])
+    ap.add_argument("--classes", type=int, default=20)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--splits", type=int, default=2, help="encode_image batch split over streams")
+    ap.add_argument("--ab-splits", action="store_true", help="also time splits=1 vs 2 (diagnostic)")
+    ap.add_argument("--ab-fold", action="store_true",
+                    help="also time a second model with MICLIP_LN_FOLD=0 in this process (diagnostic)")
+    return ap.parse_args(argv)
+
+
+# ------------------------------------------------------------------ launcher --
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_entry(rank, world, port, argv):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    run(parse(argv))
+
+
+def spawn(args, argv):
+    """One process per GPU, started before this process touches the GPU."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_entry, args=(r, args.gpus, port, argv)) for r in range(args.gpus)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join()
+    codes = [p.exitcode for p in procs]
+    if any(codes):
+        log(f"[bench] rank exit codes {codes}")
+    return max((abs(c) for c in codes if c), default=0)
+
+
+# ------------------------------------------------------------- CPU baseline --
+
 def cpu_baseline(model, cfg, budget_s=12.0, max_images=64):
     """Time the fp32 torch-CPU oracle (reference arithmetic) on a bounded sample."""
+    import torch
     from oracle import clip_oracle
     from miclip.weights import synthetic_images
     cores = len(os.sched_getaffinity(0))
@@ -76,21 +141,35 @@ def cpu_baseline(model, cfg, budget_s=12.0, max_images=64):
                       f"{threads} threads, {cpu_model}; baseline, not target"}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--model", default="ViT-L/14")
-    ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
-    ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16", "mxfp8"])
-    ap.add_argument("--classes", type=int, default=20)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--splits", type=int, default=2, help="encode_image batch split over streams")
-    ap.add_argument("--ab-splits", action="store_true", help="also time splits=1 vs 2 (diagnostic)")
-    args = ap.parse_args()
+# ---------------------------------------------------------------- roofline --
+
+def fc_epilogue(numerics):
+    """The c_fc GEMM's epilogue functor as it appears in the kernel symbol."""
+    if numerics["mxfp8"]:
+        return "EpiMX"
+    return "EpiStoreLN" if numerics["lnfold"] else "EpiStore"
+
+
+def attach_traffic(model_name, dtype, epi, M):
+    """HBM-side bytes per launch from the committed PMC profile, only when it was
+    taken on the same kernel (epilogue), model, dtype and launch shape."""
+    try:
+        with open(TRAFFIC_JSON) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None, "no profile"
+    want = {"model": model_name, "dtype": dtype, "epilogue": epi, "M": M}
+    got = {k: t.get(k) for k in want}
+    if got != want:
+        return None, f"profile is for {got}, run is {want}"
+    return t.get("hbm_bytes_per_launch"), t.get("source")
+
+
+# --------------------------------------------------------------------- rank --
+
+def run(args):
+    import torch
+    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -98,28 +177,38 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        world = dist.get_world_size()            # the group RCCL actually formed
+        rank = dist.get_rank()
+    if args.gpus != world and rank == 0:
+        log(f"[bench] --gpus {args.gpus} but the process group has {world} ranks; reporting {world}")
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
 
     import miclip
     from miclip.configs import MODEL_CONFIGS, algorithmic_gflop_per_image
+    from miclip.feature_cache import shard_range, sharded_encode
     from miclip.weights import CLIP_MEAN, CLIP_STD
     cfg = MODEL_CONFIGS[args.model]
-    B, R = args.batch, cfg.image_resolution
+    R, W = cfg.image_resolution, cfg.vision_width
+    n_global = args.batch * world if args.scaling == "weak" else args.batch
+    lo, hi = shard_range(n_global, rank, world)
     t_load = time.perf_counter()
     _, model, _ = miclip.load(args.model, device=dev, compute_dtype=args.dtype)
-    # dense MFMA peak of the GEMM operand type: MX-fp8 runs at twice the f16 rate
-    peak = PEAK_TFLOPS * (2 if args.dtype == "mxfp8" else 1)
-    model.reserve(B, args.classes)
+    peak = PEAK_TFLOPS * (2 if args.dtype == "mxfp8" else 1)   # MX-fp8 runs at 2x the f16 rate
+    model.reserve(max(hi - lo, 1), args.classes)
     model.set_splits(args.splits)
-    log(f"[rank {rank}] model loaded in {time.perf_counter() - t_load:.1f}s")
+    log(f"[rank {rank}] model loaded in {time.perf_counter() - t_load:.1f}s; "
+        f"{hi - lo} of {n_global} images per step on this rank")
 
-    # synthetic CLIP-normalised images, device-resident before timing
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    u = torch.rand(B, 3, R, R, device=dev, generator=g)
+    # the global batch of synthetic CLIP-normalised images, identical on every rank
+    # (a deterministic loader), device-resident before timing
+    g = torch.Generator(device=dev).manual_seed(1234)
     mean = torch.tensor(CLIP_MEAN, device=dev).view(1, 3, 1, 1)
     std = torch.tensor(CLIP_STD, device=dev).view(1, 3, 1, 1)
-    imgs = ((u - mean) / std).contiguous()
+    imgs = torch.empty(n_global, 3, R, R, device=dev)
+    for i in range(0, n_global, 256):
+        u = torch.rand(min(256, n_global - i), 3, R, R, device=dev, generator=g)
+        imgs[i:i + u.shape[0]] = (u - mean) / std
     del u
 
     # text head once (clip_classifier flow): synthetic prompt tokens -> encode_text
@@ -134,52 +223,81 @@ def main():
     _, temb = model.encode_text(toks.to(dev))
     tw = torch.nn.functional.normalize(temb, dim=-1).t().contiguous()      # [E, C]
 
-    feats = torch.empty(B, cfg.vision_width, device=dev)
-    gathered = torch.empty(world * B, cfg.vision_width, device=dev) if world > 1 else feats
+    def make_step(m):
+        def enc(x):
+            return m.encode_image(x, normalize=True)
 
-    def step():
-        model.encode_image(imgs, normalize=True, out=feats)
+        def step():
+            feats = sharded_encode(enc, imgs, dim=W)        # [n_global, W], global row order
+            return m.zero_shot(feats, tw, 100.0, k=1, apply_proj=True)
+        return step
+
+    step = make_step(model)
+
+    def timed(fn, steps):
+        torch.cuda.synchronize()
         if world > 1:
-            dist.all_gather_into_tensor(gathered, feats)
-        return model.zero_shot(gathered, tw, 100.0, k=1, apply_proj=True)
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        dt_t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+        return float(dt_t.item())
+
+    # correctness guard on the timed path: the gathered rows are the single-GPU encode
+    if world > 1:
+        chk = sharded_encode(lambda x: model.encode_image(x, normalize=True), imgs[:64], dim=W)
+        ref = model.encode_image(imgs[:64], normalize=True)
+        assert torch.equal(chk, ref), "sharded encode differs from the single-GPU encode"
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    dt_t = torch.tensor([dt], device=dev, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
-    dt = float(dt_t.item())
-    value = world * B * args.steps / dt
+    dt = timed(step, args.steps)
+    value = n_global * args.steps / dt
     gf = algorithmic_gflop_per_image(cfg)
 
     ab = None
     if args.ab_splits:
         ab = {}
-        for sp in (1, 2, 3, 4, 2, 3, 4):
+        for sp in (1, 2, 3, 1, 2, 3):
             model.set_splits(sp)
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            for _ in range(args.steps):
-                step()
-            torch.cuda.synchronize()
-            ab.setdefault(f"splits{sp}", []).append(round(world * B * args.steps / (time.perf_counter() - t1), 1))
+            step()
+            ab.setdefault(f"splits{sp}", []).append(round(n_global * args.steps / timed(step, args.steps), 1))
         model.set_splits(args.splits)
+    abf = None
+    if args.ab_fold:
+        prev = os.environ.get("MICLIP_LN_FOLD")
+        os.environ["MICLIP_LN_FOLD"] = "0"
+        _, m0, _ = miclip.load(args.model, device=dev, compute_dtype=args.dtype)
+        if prev is None:
+            del os.environ["MICLIP_LN_FOLD"]
+        else:
+            os.environ["MICLIP_LN_FOLD"] = prev
+        m0.reserve(max(hi - lo, 1), args.classes)
+        m0.set_splits(args.splits)
+        step0 = make_step(m0)
+        step0()
+        abf = {"fold": [], "nofold": [], "fold_flags": model.numerics(), "nofold_flags": m0.numerics()}
+        for _ in range(3):
+            abf["fold"].append(round(n_global * args.steps / timed(step, args.steps), 1))
+            abf["nofold"].append(round(n_global * args.steps / timed(step0, args.steps), 1))
+        abf["fold_median"] = statistics.median(abf["fold"])
+        abf["nofold_median"] = statistics.median(abf["nofold"])
+        del m0, step0
+        torch.cuda.empty_cache()
 
     roofline, kernels = None, None
     prof = None
     if not args.no_profile:
-        # every rank runs the profiled step: it contains the all-gather
+        # every rank runs the profiled step (it contains the all-gather); profiling
+        # runs each rank's batch unsplit on one stream, so a GEMM launch has M = b*N
         model.set_profiling(True)
         step()
         torch.cuda.synchronize()
@@ -195,39 +313,39 @@ def main():
             per_launch_s = fc["ms"] * 1e-3 / fc["launches"]
             flops_launch = fc["flops"] / fc["launches"]
             achieved = flops_launch / per_launch_s / 1e12
-            traffic = None
-            tpath = os.path.join(ROOT, "profiles", "traffic_gemm_fc.json")
-            if os.path.isfile(tpath):
-                try:
-                    with open(tpath) as f:
-                        t = json.load(f)
-                    if t.get("model") == args.model and t.get("batch") == B:
-                        traffic = t.get("hbm_bytes_per_launch")
-                except (OSError, ValueError):
-                    traffic = None
+            M = (hi - lo) * cfg.n_tokens
+            epi = fc_epilogue(model.numerics())
+            traffic, tsrc = attach_traffic(args.model, args.dtype, epi, M)
             act_name = "exact-GELU" if cfg.act == "erf" else "QuickGELU"
-            roofline = {"bound": "mfma", "kernel": f"gemm_fc (MLP c_fc + {act_name} epilogue)",
-                        "achieved": round(achieved, 1), "peak": round(peak, 1),
-                        "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                        "traffic": traffic,
+            roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": round(peak, 1),
+                        "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                        "kernel": f"gemm_fc: MLP c_fc GEMM, {epi} epilogue + {act_name}"
+                                  + (" (ln_2 folded in)" if epi == "EpiStoreLN" else ""),
+                        "launch": {"M": M, "N": 4 * W, "K": W, "splits": 1,
+                                   "timing": "HIP events on the launch stream, profiled step"},
                         "algorithmic_flops_per_launch": flops_launch,
-                        "avg_launch_ms": round(per_launch_s * 1e3, 4)}
+                        "avg_launch_ms": round(per_launch_s * 1e3, 4),
+                        "traffic_source": tsrc}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(model, cfg, budget_s=args.cpu_seconds)
 
     if rank == 0:
+        per_gpu = f"{args.batch}/GPU" if args.scaling == "weak" else f"{n_global}/{world} per GPU"
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
-            "config": {"workload": f"{args.model} feature-cache encode: encode_image bs={B}/GPU "
-                                   f"@{R}px + L2-normalise + RCCL all-gather + zero-shot "
-                                   f"logits ({args.classes} classes)",
-                       "global_batch": world * B, "tokens_per_image": cfg.n_tokens,
-                       "parallelism": f"dp{world} (image-batch sharding)",
+            "scaling": args.scaling, "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic (224px CLIP-normalised uniform noise; seeded random-init weights)",
+            "config": {"workload": f"{args.model} feature-cache encode: encode_image bs={per_gpu} "
+                                   f"@{R}px + L2-normalise + RCCL all-gather (sharded_encode) + "
+                                   f"zero-shot logits ({args.classes} classes)",
+                       "global_batch": n_global, "images_per_gpu": hi - lo,
+                       "tokens_per_image": cfg.n_tokens,
+                       "parallelism": f"dp{world} (image-batch sharding, {args.scaling} scaling)",
+                       "splits": args.splits, "numerics": model.numerics(),
                        "weights": "seeded random init, CLIP shapes"},
             "gflop_per_image": round(gf, 3),
             "path_mfma_frac": round(value * gf * 1e9 / (world * peak * 1e12), 4),
@@ -235,9 +353,19 @@ def main():
         }
         if ab:
             line["splits_ab_img_s"] = ab
+        if abf:
+            line["fold_ab_img_s"] = abf
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def main():
+    argv = sys.argv[1:]
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn(args, argv))
+    run(args)
 
 
 if __name__ == "__main__":

@@ -177,6 +177,13 @@ const char* miclip_last_error(void);
 int miclip_abi_version(void);
 /* Device-memory bytes currently held by the handle (weights + workspaces). */
 int64_t miclip_model_bytes(const miclip_model* m);
+/* Numerics path the handle runs (fixed at create; env MICLIP_RESID_F32 / MICLIP_LN_FOLD):
+ * MICLIP_MODEL_RESID16 fp16 residual stream, MICLIP_MODEL_LNFOLD ln_1 / ln_2 folded
+ * into the QKV / c_fc GEMMs, MICLIP_MODEL_MXFP8 MX-fp8 GEMM operands. 0 for NULL. */
+#define MICLIP_MODEL_RESID16 1
+#define MICLIP_MODEL_LNFOLD 2
+#define MICLIP_MODEL_MXFP8 4
+int miclip_model_flags(const miclip_model* m);
 
 /* ---- diagnostics: per-kernel-class timing with HIP events ---- */
 

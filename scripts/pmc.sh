@@ -18,7 +18,7 @@ pass() {
   if [ $rc -ne 0 ]; then echo "stopping"; exit $rc; fi
 }
 if [ "${1:-}" = traffic ]; then
-  CMD=(python3 scripts/bench_ops.py --ops gemm --only fc --variants 0 --iters 5)
+  CMD=(python3 bench.py --steps 2 --warmup 1 --splits 1 --no-cpu-baseline --no-profile)
   pass fetch FETCH_SIZE "${CMD[@]}"
   pass write WRITE_SIZE "${CMD[@]}"
   python3 scripts/traffic.py

@@ -72,3 +72,4 @@ def test_abi_version_and_validation(lib):
     assert lib.miclip_op_gemm(0, None, None, None, None, 1, 128, 64, 0, 0, 0, None) == -1
     lib.miclip_model_destroy(None)           # no-op on NULL
     assert lib.miclip_model_bytes(None) == 0
+    assert lib.miclip_model_flags(None) == 0
