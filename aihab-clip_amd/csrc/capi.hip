@@ -577,68 +577,104 @@ int miclip_model_create(const miclip_config* cfg, int device, miclip_model** out
   return 0;
 }
 
-int miclip_model_load_weights(miclip_model* m, const miclip_tensor* t, int32_t n) {
+}  // extern "C"
+
+namespace {
+
+// Copies / repacks the named fp32 tensors; `device_src`: t[i].data are device
+// pointers on the handle's device (no host round trip), else host pointers.
+// GEMM weights are cast (and conv1 padded) on the device from one fp32 staging
+// upload -- or straight from the caller's device tensor.
+int load_weights(miclip_model* m, const miclip_tensor* t, int32_t n, bool device_src) {
   if (!m || (!t && n)) return fail(MICLIP_EINVAL, "null argument");
   MICLIP_HIP(hipSetDevice(m->device));
   m->folded[0] = m->folded[1] = false;
-  std::vector<uint16_t> tmp;
+  const hipMemcpyKind kind = device_src ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  void* stage = nullptr;
+  size_t stage_bytes = 0;
+  auto done = [&](int rc) {
+    if (stage) {
+      (void)hipDeviceSynchronize();
+      dev_free(m, stage);
+    }
+    return rc;
+  };
   for (int i = 0; i < n; ++i) {
-    if (!t[i].name || !t[i].data) return fail(MICLIP_EINVAL, "null tensor name/data");
+    if (!t[i].name || !t[i].data) return done(fail(MICLIP_EINVAL, "null tensor name/data"));
     auto it = m->slots.find(t[i].name);
     if (it == m->slots.end())
-      return fail(MICLIP_EINVAL, std::string("unexpected key in state_dict: ") + t[i].name);
+      return done(fail(MICLIP_EINVAL, std::string("unexpected key in state_dict: ") + t[i].name));
     auto& slot = it->second;
     if (t[i].numel != slot.numel)
-      return fail(MICLIP_EINVAL, std::string("size mismatch for ") + t[i].name + ": got " +
-                                     std::to_string(t[i].numel) + ", expected " +
-                                     std::to_string(slot.numel));
+      return done(fail(MICLIP_EINVAL, std::string("size mismatch for ") + t[i].name + ": got " +
+                                          std::to_string(t[i].numel) + ", expected " +
+                                          std::to_string(slot.numel)));
     int rc;
     if (slot.kind == 0) {
-      if (!*slot.dst && (rc = dev_alloc(m, slot.dst, (size_t)slot.numel * 4))) return rc;
-      MICLIP_HIP(hipMemcpy(*slot.dst, t[i].data, (size_t)slot.numel * 4, hipMemcpyHostToDevice));
-    } else {
-      int64_t rows = 0, cols = 0, src_cols = 0;
-      if (slot.kind == 1) {
-        // nn.Linear / in_proj weight [out, in]: already the W[N][K] operand layout
-        const std::string nm = it->first;
-        const bool is_cproj = nm.find("c_proj") != std::string::npos;
-        const int W = slot.visual ? m->cfg.vision_width : m->cfg.transformer_width;
-        cols = is_cproj ? 4 * W : W;
-        rows = slot.numel / cols;
-        src_cols = cols;
-      } else {
-        // conv1.weight [W, 3, P, P] -> [W, Kp] zero-padded (col = c*P*P + ky*P + kx)
-        const int P = m->cfg.vision_patch_size;
-        rows = m->cfg.vision_width;
-        src_cols = 3 * P * P;
-        cols = m->Kp;
-      }
-      if (slot.sdst) {
-        // MX-fp8 weight: fp32 rows quantised on the device (quant_mx, gemm_mx.hip)
-        const size_t nb = (size_t)rows * cols;
-        if (!*slot.dst && (rc = dev_alloc(m, slot.dst, nb))) return rc;
-        if (!*slot.sdst && (rc = dev_alloc(m, slot.sdst, mx_scale_bytes(rows, cols)))) return rc;
-        void* stage = nullptr;
-        if ((rc = dev_alloc(m, &stage, nb * 4))) return rc;
-        MICLIP_HIP(hipMemcpy(stage, t[i].data, nb * 4, hipMemcpyHostToDevice));
-        MICLIP_HIP(quant_mx(0, stage, (int)rows, (int)cols, *slot.dst, *slot.sdst, nullptr));
-        MICLIP_HIP(hipDeviceSynchronize());
-        dev_free(m, stage);
-        slot.loaded = true;
-        continue;
-      }
-      tmp.assign((size_t)rows * cols, 0);
-      for (int64_t r = 0; r < rows; ++r)
-        for (int64_t c = 0; c < src_cols; ++c) {
-          const float v = t[i].data[r * src_cols + c];
-          tmp[r * cols + c] = m->dtype == MICLIP_FP16 ? f32_to_f16_bits(v) : f32_to_bf16_bits(v);
-        }
-      if (!*slot.dst && (rc = dev_alloc(m, slot.dst, tmp.size() * 2))) return rc;
-      MICLIP_HIP(hipMemcpy(*slot.dst, tmp.data(), tmp.size() * 2, hipMemcpyHostToDevice));
+      if (!*slot.dst && (rc = dev_alloc(m, slot.dst, (size_t)slot.numel * 4))) return done(rc);
+      MICLIP_HIP(hipMemcpy(*slot.dst, t[i].data, (size_t)slot.numel * 4, kind));
+      slot.loaded = true;
+      continue;
     }
+    int64_t rows = 0, cols = 0, src_cols = 0;
+    if (slot.kind == 1) {
+      // nn.Linear / in_proj weight [out, in]: already the W[N][K] operand layout
+      const bool is_cproj = it->first.find("c_proj") != std::string::npos;
+      const int W = slot.visual ? m->cfg.vision_width : m->cfg.transformer_width;
+      cols = is_cproj ? 4 * W : W;
+      rows = slot.numel / cols;
+      src_cols = cols;
+    } else {
+      // conv1.weight [W, 3, P, P] -> [W, Kp] zero-padded (col = c*P*P + ky*P + kx)
+      const int P = m->cfg.vision_patch_size;
+      rows = m->cfg.vision_width;
+      src_cols = 3 * P * P;
+      cols = m->Kp;
+    }
+    // fp32 source rows on the device
+    const float* src = t[i].data;
+    const size_t src_bytes = (size_t)slot.numel * 4;
+    if (!device_src) {
+      if (src_bytes > stage_bytes) {
+        if (stage) {
+          MICLIP_HIP(hipDeviceSynchronize());
+          dev_free(m, stage);
+          stage = nullptr;
+        }
+        if ((rc = dev_alloc(m, &stage, src_bytes))) return done(rc);
+        stage_bytes = src_bytes;
+      }
+      MICLIP_HIP(hipMemcpy(stage, t[i].data, src_bytes, hipMemcpyHostToDevice));
+      src = (const float*)stage;
+    }
+    if (slot.sdst) {
+      // MX-fp8 weight: fp32 rows quantised on the device (quant_mx, gemm_mx.hip)
+      const size_t nb = (size_t)rows * cols;
+      if (!*slot.dst && (rc = dev_alloc(m, slot.dst, nb))) return done(rc);
+      if (!*slot.sdst && (rc = dev_alloc(m, slot.sdst, mx_scale_bytes(rows, cols)))) return done(rc);
+      MICLIP_HIP(quant_mx(0, src, (int)rows, (int)cols, *slot.dst, *slot.sdst, nullptr));
+    } else {
+      if (!*slot.dst && (rc = dev_alloc(m, slot.dst, (size_t)rows * cols * elt()))) return done(rc);
+      MICLIP_HIP(cast_pad(m->dtype, src, *slot.dst, rows, (int)src_cols, (int)cols, nullptr));
+    }
+    // the next upload reuses the staging buffer: finish this conversion first
+    if (!device_src) MICLIP_HIP(hipStreamSynchronize(nullptr));
     slot.loaded = true;
   }
-  return 0;
+  if (device_src) MICLIP_HIP(hipDeviceSynchronize());
+  return done(0);
+}
+
+}  // namespace
+
+extern "C" {
+
+int miclip_model_load_weights(miclip_model* m, const miclip_tensor* t, int32_t n) {
+  return load_weights(m, t, n, false);
+}
+
+int miclip_model_load_weights_device(miclip_model* m, const miclip_tensor* t, int32_t n) {
+  return load_weights(m, t, n, true);
 }
 
 int miclip_reserve(miclip_model* m, int32_t max_images, int32_t max_prompts) {

@@ -247,6 +247,35 @@ __global__ __launch_bounds__(64) void row_l2norm_kernel(float* __restrict__ x, i
 
 }  // namespace
 
+// Weight repack at load (convert_weights, clip/model.py:372-393): fp32 rows
+// [rows, src_cols] -> compute dtype [rows, cols], zero-padded columns
+// (conv1's 3P^2 -> Kp). Round to nearest even, like the reference's .half().
+template <typename T>
+__global__ __launch_bounds__(256) void cast_pad_kernel(const float* __restrict__ in,
+                                                       T* __restrict__ out, int64_t rows,
+                                                       int src_cols, int cols) {
+  const int64_t n = rows * cols;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / cols;
+    const int c = (int)(i - r * cols);
+    out[i] = (T)(c < src_cols ? in[r * src_cols + c] : 0.f);
+  }
+}
+
+hipError_t cast_pad(int dtype, const float* in, void* out, int64_t rows, int src_cols, int cols,
+                    hipStream_t s) {
+  if (!in || !out || rows < 1 || src_cols < 1 || cols < src_cols) return hipErrorInvalidValue;
+  const int64_t n = rows * cols;
+  const int grid = (int)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  if (dtype == kF16)
+    hipLaunchKernelGGL((cast_pad_kernel<_Float16>), dim3(grid), dim3(256), 0, s, in,
+                       (_Float16*)out, rows, src_cols, cols);
+  else
+    hipLaunchKernelGGL((cast_pad_kernel<__bf16>), dim3(grid), dim3(256), 0, s, in, (__bf16*)out,
+                       rows, src_cols, cols);
+  return hipGetLastError();
+}
+
 hipError_t row_l2norm(float* x, int R, int D, hipStream_t s) {
   if (R < 1 || D < 1) return hipErrorInvalidValue;
   hipLaunchKernelGGL(row_l2norm_kernel, dim3(R), dim3(64), 0, s, x, D);

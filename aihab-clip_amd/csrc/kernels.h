@@ -103,6 +103,9 @@ hipError_t token_embed(const int64_t* tokens, const float* tok_emb, const float*
 // out[r, :] = in[r, :] @ Wm  (fp32, Wm [D, E] row-major)
 hipError_t rowvec_matmul(const float* in, const float* Wm, float* out, int R, int D, int E,
                          hipStream_t s);
+// fp32 [rows, src_cols] -> compute dtype [rows, cols] (cols >= src_cols, zero pad), RNE
+hipError_t cast_pad(int dtype, const float* in, void* out, int64_t rows, int src_cols, int cols,
+                    hipStream_t s);
 // in-place row L2 normalisation (F.normalize, eps 1e-12), fp32 [R, D]
 hipError_t row_l2norm(float* x, int R, int D, hipStream_t s);
 // zero-shot head: f = normalize(x @ proj) (proj may be null -> f = normalize(x));

@@ -23,7 +23,8 @@ MICLIP_MODEL_LNFOLD = 2
 MICLIP_MODEL_MXFP8 = 4
 
 EXPORTS = (
-    "miclip_model_create", "miclip_model_load_weights", "miclip_reserve",
+    "miclip_model_create", "miclip_model_load_weights", "miclip_model_load_weights_device",
+    "miclip_reserve",
     "miclip_encode_image", "miclip_encode_text", "miclip_zero_shot",
     "miclip_model_destroy", "miclip_last_error", "miclip_abi_version",
     "miclip_model_bytes", "miclip_model_flags", "miclip_set_profiling", "miclip_profile_read", "miclip_set_splits",
@@ -80,6 +81,7 @@ def load_library(path: str = None):
     sig = {
         "miclip_model_create": ([ctypes.POINTER(MiclipConfig), ctypes.c_int, ctypes.POINTER(vp)], ctypes.c_int),
         "miclip_model_load_weights": ([vp, ctypes.POINTER(MiclipTensor), i32], ctypes.c_int),
+        "miclip_model_load_weights_device": ([vp, ctypes.POINTER(MiclipTensor), i32], ctypes.c_int),
         "miclip_reserve": ([vp, i32, i32], ctypes.c_int),
         "miclip_encode_image": ([vp, vp, i32, vp, u32, vp], ctypes.c_int),
         "miclip_encode_text": ([vp, vp, i32, vp, vp, vp], ctypes.c_int),

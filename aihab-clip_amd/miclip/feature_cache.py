@@ -182,7 +182,7 @@ def compute_image_features_test(clip_model, loader, proj, text_weights):
     device = _model_device(clip_model)
     hits = []
     for images, target in loader:
-        x = clip_model.encode_image(images.to(device))
+        x = clip_model.encode_image(prepare_images(clip_model, images, device))
         f = proj(x) if callable(proj) and not isinstance(proj, torch.Tensor) else x @ proj.to(x)
         _, top = clip_model.zero_shot(f, text_weights, 100.0, k=1, apply_proj=False)
         hits += (top[:, 0].cpu() == target.cpu()).tolist()
@@ -265,6 +265,9 @@ def cache_preprojection_features(cfg, clip_bundle: dict, dl_tr, info: dict):
     clip_model = clip_bundle["clip_model"]
     cache_dir = _feature_cache_dir(cfg)
     num_views = int(cfg.get("aug_views", 1) or 1)
+    expected_n = info.get("train_size") if info else None
+    if expected_n is None and hasattr(dl_tr, "dataset"):
+        expected_n = len(dl_tr.dataset)
     clip_model.eval()
     for v in range(num_views):
         feats_t, labels_t = compute_image_features(clip_model, dl_tr, to_cpu=True)
@@ -275,7 +278,8 @@ def cache_preprojection_features(cfg, clip_bundle: dict, dl_tr, info: dict):
             torch.save(labels_t, cache_dir / "label.pth")
         loaded = torch.load(fpath, map_location="cpu", weights_only=True)
         print({"view": v, "reload_shape_ok": tuple(loaded.shape) == tuple(feats_t.shape),
-               "rows_match_labels": feats_t.shape[0] == labels_t.shape[0]})
+               "rows_match_labels": feats_t.shape[0] == labels_t.shape[0],
+               "rows_match_expected": expected_n is None or feats_t.shape[0] == int(expected_n)})
     return cache_dir
 
 

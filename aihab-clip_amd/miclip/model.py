@@ -73,6 +73,22 @@ class _Handle:
         _lib.check(self.lib.miclip_model_load_weights(self.ptr, arr, len(named_arrays)),
                    "miclip_model_load_weights")
 
+    def load_device(self, named_tensors):
+        """Device fp32 tensors on this handle's device: no host round trip."""
+        keep = []
+        arr = (_lib.MiclipTensor * len(named_tensors))()
+        for i, (name, t) in enumerate(named_tensors):
+            t = t.detach().to(torch.float32).contiguous()
+            if t.device.type != "cuda" or t.device.index != self.device_index:
+                raise ValueError(f"{name}: expected a tensor on cuda:{self.device_index}, got {t.device}")
+            keep.append(t)
+            arr[i].name = name.encode()
+            arr[i].data = t.data_ptr()
+            arr[i].numel = t.numel()
+        torch.cuda.synchronize(self.device_index)      # the tensors' producers are done
+        _lib.check(self.lib.miclip_model_load_weights_device(self.ptr, arr, len(named_tensors)),
+                   "miclip_model_load_weights_device")
+
     def close(self):
         if self.ptr:
             self.lib.miclip_model_destroy(self.ptr)
@@ -136,14 +152,13 @@ class CLIP(nn.Module):
         if self._handle is not None:
             self._handle.close()
         h = _Handle(self.config, _DTYPES[self.compute_dtype][0], idx)
-        h.load([(k, v.detach().float().cpu().numpy()) for k, v in self.state_dict().items()])
+        h.load_device(list(self.state_dict().items()))
         self._handle = h
 
     def refresh_weights(self):
-        """Re-upload Parameters after they were modified in place."""
+        """Re-upload Parameters after they were modified in place (device to device)."""
         if self._handle is not None:
-            self._handle.load([(k, v.detach().float().cpu().numpy())
-                               for k, v in self.state_dict().items()])
+            self._handle.load_device(list(self.state_dict().items()))
 
     # -- reference surface ---------------------------------------------------
     @property

@@ -84,6 +84,11 @@ int miclip_model_create(const miclip_config* cfg, int device, miclip_model** out
  * weights in the compute dtype, LayerNorm/bias/embeddings fp32). May be called
  * several times; unknown names are an error, "logit_scale" is accepted and unused. */
 int miclip_model_load_weights(miclip_model* m, const miclip_tensor* tensors, int32_t n);
+/* Same, with every `data` a DEVICE pointer (fp32, contiguous, on the handle's
+ * device): e.g. the model's own torch Parameters after .to(device), so a device
+ * move never round-trips the state dict through host memory. Repacking (cast to
+ * the compute dtype, conv1 padding, MX quantisation) runs on the device. */
+int miclip_model_load_weights_device(miclip_model* m, const miclip_tensor* tensors, int32_t n);
 
 /* Pre-allocates workspaces for up to max_images images / max_prompts prompts,
  * so later encode calls allocate nothing (required before hipGraph capture). */

@@ -1,7 +1,19 @@
-"""CPU, world_size 2 (gloo): image-batch sharding + all-gather reproduces the
-single-process result row for row (the multi-GPU feature cache path)."""
+"""CPU, world_size 2 (gloo): the product's sharded feature-cache path
+(miclip.feature_cache.compute_image_features_sharded -> sharded_encode ->
+all_gather_into_tensor) reproduces the single-process compute_image_features
+row for row (row order aihab_utils/feature_cache.py:144-162),
+including batches smaller than the world (a rank with an empty shard).
+
+The HIP model needs a GPU, so the encoder here is a deterministic stand-in with
+the model surface the drivers use (parameters() for device inference,
+config.vision_width, encode_image(x, normalize=...)); its rows depend on their
+own image only, like the real encoder (checked bitwise on the GPU by
+tests/test_gpu_parity.py::test_batch_invariance_and_shards and
+tests/test_gpu_distributed.py).
+"""
 import os
 import socket
+from types import SimpleNamespace
 
 import pytest
 import torch
@@ -17,38 +29,66 @@ def _free_port():
     return p
 
 
-def _encode(x):
-    # stand-in encoder (the C ABI needs a GPU): a fixed nonlinear row map + L2 norm
-    w = torch.linspace(-1, 1, x[0].numel()).view(-1, 1) * torch.arange(1, 9).view(1, -1)
-    return torch.nn.functional.normalize(torch.tanh(x.flatten(1) @ w), dim=-1)
+class StubCLIP(torch.nn.Module):
+    """Row-wise encoder: a fixed nonlinear map of each image + optional L2 norm."""
+
+    def __init__(self, width=8):
+        super().__init__()
+        self.config = SimpleNamespace(vision_width=width)
+        self.w = torch.nn.Parameter(torch.linspace(-1, 1, 3 * 4 * 4).view(-1, 1) *
+                                    torch.arange(1, width + 1).view(1, -1), requires_grad=False)
+
+    @torch.no_grad()
+    def encode_image(self, x, normalize=False):
+        y = torch.tanh(x.flatten(1) @ self.w)
+        return torch.nn.functional.normalize(y, dim=-1) if normalize else y
 
 
-def _worker(rank, world, port, n, q):
+def _batches(sizes):
+    g = torch.Generator().manual_seed(0)
+    out, label = [], 0
+    for n in sizes:
+        out.append((torch.randn(n, 3, 4, 4, generator=g), torch.arange(label, label + n)))
+        label += n
+    return out
+
+
+def _worker(rank, world, port, sizes, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from miclip.feature_cache import sharded_encode
-    g = torch.Generator().manual_seed(0)
-    images = torch.randn(n, 3, 4, 4, generator=g)
-    out = sharded_encode(_encode, images, dim=8)
-    q.put((rank, out.numpy()))
+    from miclip.feature_cache import compute_image_features_sharded, sharded_encode
+    model = StubCLIP()
+    feats, labels = compute_image_features_sharded(model, _batches(sizes), normalize=True)
+    one = sharded_encode(lambda x: model.encode_image(x), torch.randn(1, 3, 4, 4), dim=8)
+    q.put((rank, feats.numpy(), labels.numpy(), str(feats.device), str(one.device), tuple(one.shape)))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [6, 7, 1])
-def test_sharded_encode_matches_single_process(n):
+@pytest.mark.parametrize("sizes", [[6, 7, 1], [1], [5, 2, 3]])
+def test_sharded_feature_cache_matches_single_process(sizes):
+    from miclip.feature_cache import compute_image_features
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     world, port = 2, _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, sizes, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(world))
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=120)
+        res[r[0]] = r[1:]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    g = torch.Generator().manual_seed(0)
-    ref = _encode(torch.randn(n, 3, 4, 4, generator=g)).numpy()
+    model = StubCLIP()
+    ref_f, ref_l = compute_image_features(
+        SimpleNamespace(parameters=model.parameters,
+                        encode_image=lambda x: model.encode_image(x, normalize=True)),
+        _batches(sizes))
     for r in range(world):
-        assert res[r].shape == ref.shape
-        assert (res[r] == ref).all()
+        feats, labels, fdev, onedev, oneshape = res[r]
+        assert fdev == "cpu" and onedev == "cpu" and oneshape == (1, 8)
+        assert feats.shape == tuple(ref_f.shape)
+        assert (feats == ref_f.numpy()).all(), "gathered rows differ from the single-process cache"
+        assert (labels == ref_l.numpy()).all()

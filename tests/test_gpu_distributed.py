@@ -1,0 +1,48 @@
+"""RCCL (torch.distributed "nccl" on ROCm) path of the sharded feature cache on the GPU box:
+a world_size-1 process group over the real HIP model. sharded_encode /
+compute_image_features_sharded give the plain encode bit for bit,
+the collective runs on the rank's HIP device whatever device the loader's
+images are on (CPU batches here, like a DataLoader's), and the timed bench
+step uses exactly this function."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_sharded_encode_rccl_world1():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import miclip
+    from miclip.feature_cache import compute_image_features_sharded, sharded_encode
+    from miclip.weights import synthetic_images
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0,
+                            world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+        _, m, _ = miclip.load("ViT-B/32", device="cuda")
+        imgs = torch.from_numpy(synthetic_images(37, 224, seed=4))           # host batch
+        ref = m.encode_image(imgs.cuda(), normalize=True)
+        got = sharded_encode(lambda x: m.encode_image(x, normalize=True), imgs, dim=768)
+        assert got.device.type == "cuda" and torch.equal(got, ref)
+        got_dev = sharded_encode(lambda x: m.encode_image(x, normalize=True), imgs.cuda(), dim=768)
+        assert torch.equal(got_dev, ref)
+        loader = [(imgs[i:i + 10], torch.arange(i, min(i + 10, 37))) for i in range(0, 37, 10)]
+        feats, labels = compute_image_features_sharded(m, loader, normalize=True)
+        assert torch.equal(feats, ref) and torch.equal(labels.cpu(), torch.arange(37))
+    finally:
+        dist.destroy_process_group()
