@@ -37,6 +37,22 @@ namespace {
 
 constexpr float kLog2e = 1.4426950408889634f;
 
+// x (op) x of lane l ^ 32, for every lane: one v_permlane32_swap (gfx950) swaps
+// the upper half of one copy with the lower half of the other, so the pair
+// {r[0], r[1]} is {x_l, x_(l^32)} in some order. A VALU op; __shfl_xor(x, 32)
+// lowers to an LDS ds_bpermute round trip in the middle of every key tile's
+// softmax (cdna_hip_programming.md T12).
+MICLIP_DEV float xor32_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+MICLIP_DEV float xor32_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  // same order on both halves (lane l < 32 sees {x_l, x_l+32}, l >= 32 {x_l-32, x_l}):
+  // the low half's value first, so both lanes of a pair hold the identical sum
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // LDS geometry of one (image, head)'s K or V image for head dim DH.
 // DH = 64: 128-B rows of 8 16-B chunks, the swizzles XOR over all 8.
 // DH = 80: rows padded to 96 dims (192 B, 12 chunks); chunks 0-7 swizzle as
@@ -128,7 +144,7 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
 #pragma unroll
     for (int r = 4; r < 16; r += 4)
       tmax = fmaxf(tmax, fmaxf(fmaxf(sacc[r], sacc[r + 1]), fmaxf(sacc[r + 2], sacc[r + 3])));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * c2;
+    tmax = xor32_max(tmax) * c2;
     // Lazy rescale (cdna_hip_programming.md T13, textbook order: the decision
     // precedes this tile's exponentials): keep the old max while the tile max
     // exceeds it by <= 8 (p <= 2^8, exact range for fp16/bf16 P).
@@ -188,7 +204,7 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
     softmax_pv(kt + 1, sb);
   }
   if (kt < nkt) softmax_pv(kt, sa);
-  lsum += __shfl_xor(lsum, 32, 64);
+  lsum = xor32_sum(lsum);
 }
 
 template <typename T, int DH>

@@ -773,6 +773,34 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
 template <class Epi> struct EpiStores { static constexpr int n = 32; };   // 4 passes x 8 rows
 template <> struct EpiStores<EpiNull> { static constexpr int n = 0; };
 
+// {mean, rstd} of rows r0, r0+8, ..., r0+56 (wave-uniform r0, all in bounds) by
+// scalar loads: SGPR results, the lgkm counter only -- a vector load here would
+// make hipcc wait vmcnt(0), draining the next tile's LDS-DMA prefetch and the
+// previous pass's stores. Reads only (nothing is written through the scalar cache).
+MICLIP_DEV void sload_stats8(const float2* r0, float2 (&st)[8]) {
+  const unsigned long long a = (unsigned long long)r0;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  const unsigned long long base = ((unsigned long long)hi << 32) | lo;
+  unsigned long long v0, v1, v2, v3, v4, v5, v6, v7;
+  asm volatile(
+      "s_load_dwordx2 %0, %8, 0x0\n\t"
+      "s_load_dwordx2 %1, %8, 0x40\n\t"
+      "s_load_dwordx2 %2, %8, 0x80\n\t"
+      "s_load_dwordx2 %3, %8, 0xc0\n\t"
+      "s_load_dwordx2 %4, %8, 0x100\n\t"
+      "s_load_dwordx2 %5, %8, 0x140\n\t"
+      "s_load_dwordx2 %6, %8, 0x180\n\t"
+      "s_load_dwordx2 %7, %8, 0x1c0\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&s"(v0), "=&s"(v1), "=&s"(v2), "=&s"(v3), "=&s"(v4), "=&s"(v5), "=&s"(v6), "=&s"(v7)
+      : "s"(base)
+      : "memory");
+  const unsigned long long v[8] = {v0, v1, v2, v3, v4, v5, v6, v7};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) st[k] = __builtin_bit_cast(float2, v[k]);
+}
+
 MICLIP_DEV void wait_vmcnt_tile(int n) {
   switch (n) {
     case 36: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
@@ -791,11 +819,10 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
   constexpr int EPI_LD = 260;            // fp32 row stride of the epilogue staging
   constexpr int STG = 4 * HALF;          // staging: 64 rows in the buffer-1 half onward
   constexpr int SMEM0 = 8 * HALF > STG + 64 * EPI_LD * 4 ? 8 * HALF : STG + 64 * EPI_LD * 4;
-  // folded LayerNorm (EpiStoreLN): the tile's 256 row statistics after the staging
-  constexpr int SMEM = SMEM0 + (IsLN<Epi>::value ? 256 * 8 + 256 * 4 : 0);
+  // folded LayerNorm (EpiStoreLN): the tile's column sums after the staging
+  constexpr int SMEM = SMEM0 + (IsLN<Epi>::value ? 256 * 4 : 0);
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
-  float2* lnst = (float2*)(smem + SMEM0);              // [256] {mean, rstd}
-  float4* lncs = (float4*)(smem + SMEM0 + 256 * 8);    // [64] column sums
+  float4* lncs = (float4*)(smem + SMEM0);              // [64] column sums
 
   const int ntn = N / 256, ntm = ntm_dp, ndp = ntm * ntn, nk = K / 64;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -936,13 +963,12 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
     const float4 bv = epi.bias4nb(cn0 + ec);   // branch-free (null bias -> zeros)
     asm volatile("" ::"v"(bv.x), "v"(bv.y), "v"(bv.z), "v"(bv.w));
     if constexpr (IsLN<Epi>::value) {
-      // the tile's row statistics and column sums, retired here like the bias
-      // and parked in LDS (read after the first pass's barrier)
+      // the tile's column sums, retired here like the bias and parked in LDS
+      // (read after the first pass's barrier). The row statistics are wave-
+      // uniform per output row (a wave stores whole rows) and come in by
+      // scalar loads in the passes below.
       const float4 sv = epi.colsum4nb(cn0 + ec);
-      const int sr = cm0 + (tid & 255);
-      const float2 st = epi.stats[sr < M ? sr : M - 1];
-      asm volatile("" ::"v"(sv.x), "v"(sv.y), "v"(sv.z), "v"(sv.w), "v"(st.x), "v"(st.y));
-      if (tid < 256) lnst[tid] = st;
+      asm volatile("" ::"v"(sv.x), "v"(sv.y), "v"(sv.z), "v"(sv.w));
       if (tid < 64) lncs[tid] = sv;
     }
     const int nid = id + gridDim.x;
@@ -994,31 +1020,69 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
       }
       lds_barrier();
       if constexpr (IsLN<Epi>::value) {
-        // two rows' worth of LDS reads in flight: the row statistics would
-        // otherwise push the fully unrolled loop past 256 VGPRs (spills)
+        // row k of this wave is cm0 + p*64 + wave + 8k for all its lanes: its
+        // {mean, rstd} is a scalar load (SGPRs, no LDS round trip, no VGPRs),
+        // so the 8 rows unroll fully and their staging reads overlap
         const float4 cs = lncs[tid & 63];
+        if (full) {
+          float2 st[8];
+          sload_stats8(epi.stats + cm0 + p * 64 + wave, st);
+          // 4 staged rows read back-to-back, one wait, then their math and stores
+          // (hipcc otherwise waits out each read's latency right before its row)
+#pragma unroll
+          for (int k0 = 0; k0 < 8; k0 += 4) {
+            f32x4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = *(const f32x4*)(stg + (wave + 8 * (k0 + k)) * EPI_LD + ec);
+            asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              epi.put4ln(cm0 + p * 64 + wave + 8 * (k0 + k), cn0 + ec,
+                         make_float4(v[k][0], v[k][1], v[k][2], v[k][3]), bv, cs, st[k0 + k]);
+          }
+        } else {
+          // partial tile (rare): clamped vector loads, rows past M skipped
 #pragma unroll 2
-        for (int k = 0; k < 8; ++k) {
-          const int lr = (tid >> 6) + 8 * k;
-          const int row = cm0 + p * 64 + lr;
-          if (full || row < M)
-            epi.put4ln(row, cn0 + ec, *(const float4*)(stg + lr * EPI_LD + ec), bv, cs,
-                       lnst[p * 64 + lr]);
+          for (int k = 0; k < 8; ++k) {
+            const int lr = wave + 8 * k;
+            const int row = cm0 + p * 64 + lr;
+            if (row < M)
+              epi.put4ln(row, cn0 + ec, *(const float4*)(stg + lr * EPI_LD + ec), bv, cs,
+                         epi.stats[row]);
+          }
         }
       }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        if constexpr (IsLN<Epi>::value) break;
-        const int lr = (tid >> 6) + 8 * k;
-        const int row = cm0 + p * 64 + lr;
-        if (full || row < M) {
-          const float4 v = *(const float4*)(stg + lr * EPI_LD + ec);
+      if constexpr (!IsLN<Epi>::value) {
+        auto emit = [&](int k, float4 v) {
+          const int row = cm0 + p * 64 + wave + 8 * k;
           if constexpr (PrefetchX<Epi>::value)
             epi.put4x(row, cn0 + ec, v, bv, xr[k]);
           else if constexpr (PrefetchXF<Epi>::value)
             epi.put4xf(row, cn0 + ec, v, bv, xf[k]);
           else
             epi.put4(row, cn0 + ec, v, bv);
+        };
+        if (full) {
+          // unguarded: 4 staged rows read back-to-back, one wait, then their
+          // math and stores (a per-row guard makes hipcc branch per row and
+          // wait out each read's latency right before it)
+#pragma unroll
+          for (int k0 = 0; k0 < 8; k0 += 4) {
+            f32x4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              v[k] = *(const f32x4*)(stg + (wave + 8 * (k0 + k)) * EPI_LD + ec);
+            asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              emit(k0 + k, make_float4(v[k][0], v[k][1], v[k][2], v[k][3]));
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int lr = wave + 8 * k;
+            if (cm0 + p * 64 + lr < M) emit(k, *(const float4*)(stg + lr * EPI_LD + ec));
+          }
         }
       }
       if constexpr (PrefetchX<Epi>::value) {   // retire every residual load on every path

@@ -35,6 +35,18 @@ if [ "${1:-}" = attn ]; then
   done
   exit 0
 fi
+if [ "${1:-}" = bench ]; then
+  # every kernel of the benched step (one unsplit step: --splits 1)
+  CMD=(python3 bench.py --steps 1 --warmup 0 --splits 1 --no-cpu-baseline --no-profile)
+  i=0
+  for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
+             "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_SALU" \
+             "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM" ; do
+    i=$((i+1))
+    pass "b$i" "$grp" "${CMD[@]}"
+  done
+  exit 0
+fi
 CMD=(python3 scripts/bench_ops.py --ops gemm --only fc,proj --variants 0 --iters 5)
 i=0
 for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
