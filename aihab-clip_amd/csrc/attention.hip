@@ -78,7 +78,7 @@ struct HeadGeom {
 // of this lane's query; attend_store writes the normalised rows.
 // kt0 / kt_end: key-tile range (kt_end < 0: all tiles the chunk attends to);
 // m: the running max (scaled log2 domain) that lsum and O^T are relative to.
-template <typename T, bool CAUSAL, int DH>
+template <typename T, bool CAUSAL, int DH, bool PIPE = true>
 MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
                              const i16x8 (&qf)[HeadGeom<DH>::NKS], int chunk, int N, int Npad,
                              float c2, int lane, f32x16 (&o)[HeadGeom<DH>::NDT], float& lsum,
@@ -194,16 +194,26 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
     }
     if (prio) __builtin_amdgcn_s_setprio(0);
   };
-  f32x16 sa, sb;
-  int kt = kt0;
-  if (kt < nkt) qk(kt, sa);
-  for (; kt + 2 <= nkt; kt += 2) {
-    qk(kt + 1, sb);
-    softmax_pv(kt, sa);
-    if (kt + 2 < nkt) qk(kt + 2, sa);
-    softmax_pv(kt + 1, sb);
+  if constexpr (PIPE) {
+    f32x16 sa, sb;
+    int kt = kt0;
+    if (kt < nkt) qk(kt, sa);
+    for (; kt + 2 <= nkt; kt += 2) {
+      qk(kt + 1, sb);
+      softmax_pv(kt, sa);
+      if (kt + 2 < nkt) qk(kt + 2, sa);
+      softmax_pv(kt + 1, sb);
+    }
+    if (kt < nkt) softmax_pv(kt, sa);
+  } else {
+    // one score tile live (16 fewer VGPRs): for kernels whose latency hiding
+    // comes from more waves per SIMD instead of the in-wave pipeline
+    f32x16 sa;
+    for (int kt = kt0; kt < nkt; ++kt) {
+      qk(kt, sa);
+      softmax_pv(kt, sa);
+    }
   }
-  if (kt < nkt) softmax_pv(kt, sa);
   lsum = xor32_sum(lsum);
 }
 
@@ -435,6 +445,115 @@ __global__ __launch_bounds__(SPLIT ? 512 : 640) void attention_pipe_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Two workgroups per CU (variant 8, default for 8 full query chunks and at most
+// 3 more queries, N in 256..259: ViT-L/14 at 224 px). One workgroup = 8 waves (2 per
+// SIMD) walks hpw (image, head) pairs with ONE K/V buffer (Npad x 256 B, 72 KiB
+// at N = 257), so two workgroups share a CU: while one stages its next head's
+// K/V (LDS-DMA) the other computes, and 4 waves per SIMD hide the softmax /
+// LDS latencies that 2-3 waves of one workgroup leave exposed (the register
+// budget is 128 VGPRs: __launch_bounds__(512, 4)). Wave w owns query chunk w
+// (8 x 32 queries) and, flash-decoding style, key tiles [w*T/8, (w+1)*T/8) of
+// the ragged last chunk (N - 256 queries: the 257th token); its partial
+// (m, l, o) per valid query goes to LDS and, after the head's closing
+// barrier, wave v merges queries v, v+8, ... in a fixed order.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restrict__ qkv,
+                                                             T* __restrict__ out, int B, int N,
+                                                             int H, int Npad, int hpw,
+                                                             float qk_scale, int prio) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int img_bytes = Npad * 128;
+  char* kimg = smem;
+  char* vimg = smem + img_bytes;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ntiles = Npad >> 5;              // key tiles (= query chunks incl. the ragged one)
+  const int nvalid = N - 256;                // queries of the ragged chunk 8 (0 = none)
+  const int xkt0 = wave * ntiles / 8, xkt1 = (wave + 1) * ntiles / 8;
+  float* part = (float*)(smem + 2 * img_bytes);   // [8 waves][nvalid][66]
+  const int D = H * 64, ld = 3 * D;
+  const float c2 = qk_scale * kLog2e;
+  const int bh0 = blockIdx.x * hpw;
+  const int nh = (B * H - bh0) < hpw ? (B * H - bh0) : hpw;
+  const int pieces = Npad / 8;
+  const int prow = lane >> 3, pch = lane & 7;
+  auto head_base = [&](int bh) {
+    const int b = bh / H, h = bh - b * H;
+    return qkv + (size_t)b * N * ld + h * 64;
+  };
+  for (int j = 0; j < nh; ++j) {
+    const int bh = bh0 + j, b = bh / H, h = bh - b * H;
+    const T* base = head_base(bh);
+    // every wave finished reading the previous head's K/V and partials (the
+    // closing barrier below) before these DMAs overwrite them
+    for (int pc = wave; pc < 2 * pieces; pc += 8) {
+      const bool isv = pc >= pieces;
+      const int piece = isv ? pc - pieces : pc;
+      const int row = piece * 8 + prow;
+      const int r = row < N ? row : N - 1;   // pad rows: finite data, masked keys
+      const int lch = isv ? (pch ^ ((row & 3) << 1)) : (pch ^ ((row >> 1) & 7));
+      glds16_hidden(base + (size_t)r * ld + (isv ? 2 * D : D) + lch * 8,
+                    (isv ? vimg : kimg) + piece * 1024);
+    }
+    i16x8 qf[4];
+    load_q<T, 64>(qf, base, ld, wave, N, lane);
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
+    __builtin_amdgcn_s_barrier();
+    T* obase = out + (size_t)b * N * D + h * 64;
+    {
+      f32x16 o[2];
+      float lsum, m;
+      attend_chunk<T, false, 64, false>(kimg, vimg, qf, wave, N, Npad, c2, lane, o, lsum, m, 0,
+                                        -1, prio);
+      attend_store<T, 64>(o, lsum, wave, N, obase, D, lane);
+    }
+    if (nvalid > 0) {
+      load_q<T, 64>(qf, base, ld, 8, N, lane);
+      f32x16 o[2];
+      float lsum, m;
+      attend_chunk<T, false, 64, false>(kimg, vimg, qf, 8, N, Npad, c2, lane, o, lsum, m, xkt0,
+                                        xkt1, prio);
+      // lane (l32, hh) holds O^T rows d = (r&3) + 8*(r>>2) + 4*hh (+32 in o[1]) of query l32
+      const int l32 = lane & 31, hh = lane >> 5;
+      if (l32 < nvalid) {
+        float* pw = part + ((size_t)wave * nvalid + l32) * 66;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int d = (r & 3) + 8 * (r >> 2) + 4 * hh;
+          pw[d] = o[0][r];
+          pw[32 + d] = o[1][r];
+        }
+        if (hh == 0) {
+          pw[64] = m;
+          pw[65] = lsum;
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // merge the ragged chunk: wave v takes queries v, v+8, ...; lane = output dim
+    for (int c = wave; c < nvalid; c += 8) {
+      const float* pc = part + (size_t)c * 66;
+      float mx = -1e30f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) mx = fmaxf(mx, pc[(size_t)i * nvalid * 66 + 64]);
+      float l = 0.f, acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float* pi = pc + (size_t)i * nvalid * 66;
+        const float w = __builtin_amdgcn_exp2f(pi[64] - mx);
+        l += w * pi[65];
+        acc += w * pi[lane];
+      }
+      obase[(size_t)(256 + c) * D + lane] = to_t<T>(acc / l);
+    }
+    // the merge's partial reads finish before the next head's partial writes:
+    // those follow the next head's first barrier, which every merging wave joins
+  }
+}
+
 // MICLIP_ATTN=1 forces the one-head-per-workgroup kernel; 4 the pipelined
 // kernel with the last-chunk split (A/B comparisons).
 int attn_variant() {
@@ -502,6 +621,35 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, 
   const size_t lds = (size_t)Npad * 256;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (variant == 0) variant = attn_variant();
+  // two workgroups per CU (default when the queries are 8 full chunks + a small
+  // ragged one: K/V (72 KiB) plus the partials of 8 waves x the ragged queries
+  // must stay under 80 KiB of LDS, i.e. N - 256 <= 3)
+  const size_t lds_x8 = lds + (size_t)8 * (N > 256 ? N - 256 : 0) * 66 * 4;
+  if (variant == 8 || (!CAUSAL && variant == 0 && N >= 256 && N < 288 && lds_x8 <= 80 * 1024)) {
+    if (CAUSAL || N < 256 || N >= 288 || lds_x8 > 80 * 1024) return hipErrorInvalidValue;
+    static bool x8_attr = false;
+    if (!x8_attr) {
+      const hipError_t e = hipFuncSetAttribute((const void*)attention_x8_kernel<T>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               80 * 1024);
+      if (e != hipSuccess) return e;
+      x8_attr = true;
+    }
+    static int ncu8 = [] {
+      int d = 0, n = 0;
+      if (hipGetDevice(&d) != hipSuccess ||
+          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+        n = 256;
+      return n;
+    }();
+    const int heads = B * H, slots = 2 * ncu8;
+    int hpw = (heads + slots - 1) / slots;
+    hpw = hpw < 1 ? 1 : hpw;
+    const int grid = (heads + hpw - 1) / hpw;
+    hipLaunchKernelGGL((attention_x8_kernel<T>), dim3(grid), dim3(512), lds_x8, s, (const T*)qkv,
+                       (T*)out, B, N, H, Npad, hpw, 0.125f, attn_prio());
+    return hipGetLastError();
+  }
   // pipelined kernel (default; variant 2): two K/V buffers must fit in LDS
   // (N <= 320). ViT-L/14 layer: 0.19-0.21 ms vs 0.21-0.24 ms one head per WG.
   if (variant != 1 && 2 * lds + 2 * 10 * 2 * 66 * 4 <= 160 * 1024) {

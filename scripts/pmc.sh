@@ -29,9 +29,9 @@ if [ "${1:-}" = attn ]; then
   i=0
   for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
              "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU" \
-             "FETCH_SIZE" "WRITE_SIZE"; do
+             "SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA SQ_INSTS_VALU_TRANS_F32"; do
     i=$((i+1))
-    pass "a$i" "$grp" "${CMD[@]}"
+    pass "b$i" "$grp" "${CMD[@]}"
   done
   exit 0
 fi

@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
-    for k in ("gemm256s_kernel", "attention_pipe_kernel", "attention_kernel", "ln_stats_kernel",
+    for k in ("gemm256s_kernel", "attention_pipe_kernel", "attention_x8_kernel", "attention_kernel", "ln_stats_kernel",
               "layernorm_h2_kernel", "layernorm_kernel", "gemm_tail", "gemm256_kernel", "im2col",
               "zero_shot", "rows_matmul", "class_token", "gemm_nt_kernel"):
         if k in name:
@@ -54,7 +54,12 @@ def main():
                "lds_per_mfma": c.get("SQ_INSTS_LDS", 0) / c["SQ_INSTS_MFMA"] if c.get("SQ_INSTS_MFMA") else None,
                "lds_idx_active_per_cu": (c.get("SQ_LDS_IDX_ACTIVE", 0) / 256) / (g / 8) if g else None,
                "lds_bank_conflict": c.get("SQ_LDS_BANK_CONFLICT", 0),
-               "wait_inst_lds_frac": c.get("SQ_WAIT_INST_LDS", 0) / wc if wc else None}
+               "wait_inst_lds_frac": c.get("SQ_WAIT_INST_LDS", 0) / wc if wc else None,
+               "active_valu_frac": c.get("SQ_ACTIVE_INST_VALU", 0) / wc if wc else None,
+               "active_lds_frac": c.get("SQ_ACTIVE_INST_LDS", 0) / wc if wc else None,
+               "active_sca_frac": c.get("SQ_ACTIVE_INST_SCA", 0) / wc if wc else None,
+               "trans_per_mfma": c.get("SQ_INSTS_VALU_TRANS_F32", 0) / c["SQ_INSTS_MFMA"] if c.get("SQ_INSTS_MFMA") else None,
+               "waves_per_simd_avg": c.get("SQ_WAVE_CYCLES", 0) / (g / 8 * 1024) if g else None}
         out[k] = {a: (round(b, 4) if isinstance(b, float) else b) for a, b in row.items()}
         print(k, json.dumps(out[k]))
     return out

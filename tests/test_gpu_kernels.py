@@ -221,6 +221,30 @@ def test_attention(lib, dt, B, N, H, causal, variant):
     assert err < (4e-2 if dt == "bf16" else 6e-3), err
 
 
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+@pytest.mark.parametrize("B,N,H", [(2, 257, 2), (37, 257, 16), (3, 256, 3), (2, 259, 2), (5, 258, 4),
+                                   (1, 257, 1)])
+def test_attention_x8(lib, dt, B, N, H):
+    """Two-workgroups-per-CU kernel (variant 8; default at N = 257): 8 full query
+    chunks + a ragged chunk split over the waves' key ranges and merged."""
+    code, tdt = DT[dt]
+    g = torch.Generator(device="cuda").manual_seed(B * 1000 + N + H + 8)
+    qkv = (torch.randn(B * N, 3 * H * 64, device="cuda", generator=g) * 1.5).to(tdt)
+    out = torch.empty(B * N, H * 64, device="cuda", dtype=tdt)
+    for variant in (8, 0):
+        out.fill_(7.0)
+        _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), out.data_ptr(), B, N, H, 64, 0,
+                                            variant, _stream()))
+        torch.cuda.synchronize()
+        ref = _attn_ref(qkv, B, N, H, 0)
+        err = (out.float() - ref).abs().max().item()
+        assert err < (4e-2 if dt == "bf16" else 6e-3), (variant, err)
+    # outside 256 <= N <= 259 (or causal) variant 8 is refused, not silently run
+    for n, causal in ((200, 0), (260, 0), (287, 0), (257, 1)):
+        assert lib.miclip_op_attention(code, qkv.data_ptr(), out.data_ptr(), 1, n, H, 64, causal, 8,
+                                       _stream()) != 0
+
+
 def test_attention_spike(lib):
     """A key row that dominates one query forces the online-softmax rescale branch."""
     B, N, H = 1, 257, 1
