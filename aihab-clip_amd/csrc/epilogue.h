@@ -126,9 +126,12 @@ struct EpiStore {
   // The fp32 result is pinned in a register before the conversion: otherwise
   // hipcc may fuse the last multiply (or add) with the conversion into one
   // v_fma_mix* (a single rounding) in some call sites and not in others, and
-  // the tile and tail paths would differ in the last bit.
+  // the tile and tail paths would differ in the last bit. Not `volatile`: an
+  // opaque op is enough to stop the fusion, and a volatile one would also pin
+  // the ORDER of all the epilogue's pins, serialising the rows' dependent
+  // exp -> rcp -> mul chains instead of interleaving them.
   MICLIP_DEV static float fin(float y) {
-    asm volatile("" : "+v"(y));
+    asm("" : "+v"(y));
     return y;
   }
   template <bool ASM = false>
@@ -144,10 +147,14 @@ struct EpiStore {
       o[2] = to_bits<T>(fin(hi[0]));
       o[3] = to_bits<T>(fin(hi[1]));
     } else {
-      o[0] = to_bits<T>(fin(act_fn<ACT>(v.x + b.x)));
-      o[1] = to_bits<T>(fin(act_fn<ACT>(v.y + b.y)));
-      o[2] = to_bits<T>(fin(act_fn<ACT>(v.z + b.z)));
-      o[3] = to_bits<T>(fin(act_fn<ACT>(v.w + b.w)));
+      // packed adds (v_pk_add_f32), the same rounding as the scalar form of put1
+      f32x2 y0 = (f32x2){v.x, v.y} + (f32x2){b.x, b.y};
+      f32x2 y1 = (f32x2){v.z, v.w} + (f32x2){b.z, b.w};
+      asm("" : "+v"(y0), "+v"(y1));
+      o[0] = to_bits<T>(y0[0]);
+      o[1] = to_bits<T>(y0[1]);
+      o[2] = to_bits<T>(y1[0]);
+      o[3] = to_bits<T>(y1[1]);
     }
     if constexpr (ASM)
       st_b64_asm(C + (size_t)r * ldc + c, o);
@@ -184,16 +191,24 @@ struct EpiStoreLN {
   MICLIP_DEV float bias1(int col) const { return bias[col]; }
   MICLIP_DEV float4 colsum4nb(int col) const { return ld_bias4_nb(colsum, col); }
   MICLIP_DEV static float fin(float y) {
-    asm volatile("" : "+v"(y));
+    asm("" : "+v"(y));
     return y;
   }
   MICLIP_DEV static float z(float v, float s, float2 st, float c) {
     return fin(__builtin_fmaf(st.y, __builtin_fmaf(-st.x, s, v), c));
   }
+  // two columns at once: the same two fused multiply-adds per element as z(),
+  // issued as packed v_pk_fma_f32 (same rounding), so tile and tail paths agree
+  MICLIP_DEV static f32x2 z2(f32x2 v, f32x2 s, float2 st, f32x2 c) {
+    const f32x2 t = __builtin_elementwise_fma((f32x2){-st.x, -st.x}, s, v);
+    f32x2 y = __builtin_elementwise_fma((f32x2){st.y, st.y}, t, c);
+    asm("" : "+v"(y));
+    return y;
+  }
   template <bool ASM = false>
   MICLIP_DEV void put4ln(int r, int c, float4 v, float4 b, float4 s, float2 st) const {
-    const f32x2 y0 = {z(v.x, s.x, st, b.x), z(v.y, s.y, st, b.y)};
-    const f32x2 y1 = {z(v.z, s.z, st, b.z), z(v.w, s.w, st, b.w)};
+    const f32x2 y0 = z2((f32x2){v.x, v.y}, (f32x2){s.x, s.y}, st, (f32x2){b.x, b.y});
+    const f32x2 y1 = z2((f32x2){v.z, v.w}, (f32x2){s.z, s.w}, st, (f32x2){b.z, b.w});
     i16x4 o;
     if constexpr (ACT == ACT_GELU || ACT == ACT_QUICKGELU) {
       const f32x2 lo = ACT == ACT_GELU ? gelu_erf2(y0) : quick_gelu2(y0);
@@ -237,7 +252,7 @@ struct EpiResidual {
   MICLIP_DEV float4 bias4nb(int col) const { return ld_bias4_nb(bias, col); }
   MICLIP_DEV float bias1(int col) const { return bias[col]; }
   MICLIP_DEV static float fin(float y) {
-    asm volatile("" : "+v"(y));
+    asm("" : "+v"(y));
     return y;
   }
   template <bool ASM = false>
@@ -267,11 +282,18 @@ struct EpiResidual {
   }
   template <bool ASM = false>
   MICLIP_DEV void put4x(int r, int c, float4 v, float4 b, i16x4 x) const {
+    // packed: (acc + b) then x + that, two v_pk_add_f32 per pair -- the same
+    // two roundings as put1's scalar form
+    const f32x2 t0 = (f32x2){v.x, v.y} + (f32x2){b.x, b.y};
+    const f32x2 t1 = (f32x2){v.z, v.w} + (f32x2){b.z, b.w};
+    f32x2 y0 = (f32x2){from_bits<R>(x[0]), from_bits<R>(x[1])} + t0;
+    f32x2 y1 = (f32x2){from_bits<R>(x[2]), from_bits<R>(x[3])} + t1;
+    asm("" : "+v"(y0), "+v"(y1));
     i16x4 o;
-    o[0] = to_bits<R>(fin(from_bits<R>(x[0]) + (v.x + b.x)));
-    o[1] = to_bits<R>(fin(from_bits<R>(x[1]) + (v.y + b.y)));
-    o[2] = to_bits<R>(fin(from_bits<R>(x[2]) + (v.z + b.z)));
-    o[3] = to_bits<R>(fin(from_bits<R>(x[3]) + (v.w + b.w)));
+    o[0] = to_bits<R>(y0[0]);
+    o[1] = to_bits<R>(y0[1]);
+    o[2] = to_bits<R>(y1[0]);
+    o[3] = to_bits<R>(y1[1]);
     i16x4* p = (i16x4*)(X + (size_t)r * ldx + c);
     if constexpr (ASM)
       st_b64_asm(p, o);
