@@ -28,7 +28,15 @@ asm: $(SRCS)
 	@mkdir -p build/asm
 	for f in $(SRCS); do $(HIPCC) $(HIPFLAGS) --cuda-device-only -S $$f -o build/asm/$$(basename $$f .hip).s; done
 
+# diagnostic libraries with in-kernel cycle stamps (scripts/stamps/run.py)
+stamps: $(OBJS)
+	@mkdir -p build/stamps
+	$(HIPCC) $(HIPFLAGS) -c scripts/stamps/stamp_gemm.hip -o build/stamps/stamp_gemm.o
+	$(HIPCC) $(HIPFLAGS) -fno-honor-nans -fno-slp-vectorize -c scripts/stamps/stamp_attn.hip -o build/stamps/stamp_attn.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) build/stamps/stamp_gemm.o $(filter-out $(OBJ_DIR)/gemm.o,$(OBJS)) -o build/stamps/libstamp_gemm.so
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) build/stamps/stamp_attn.o $(filter-out $(OBJ_DIR)/attention.o,$(OBJS)) -o build/stamps/libstamp_attn.so
+
 clean:
 	rm -rf build $(LIB)
 
-.PHONY: all clean asm
+.PHONY: all clean asm stamps

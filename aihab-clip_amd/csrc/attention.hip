@@ -483,6 +483,7 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
     const int b = bh / H, h = bh - b * H;
     return qkv + (size_t)b * N * ld + h * 64;
   };
+  MICLIP_STAMP_BEGIN;
   for (int j = 0; j < nh; ++j) {
     const int bh = bh0 + j, b = bh / H, h = bh - b * H;
     const T* base = head_base(bh);
@@ -501,13 +502,16 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
     load_q<T, 64>(qf, base, ld, wave, N, lane);
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
     __builtin_amdgcn_s_barrier();
+    MICLIP_STAMP(0);   // K/V DMA + Q loads, their wait, the barrier
     T* obase = out + (size_t)b * N * D + h * 64;
     {
       f32x16 o[2];
       float lsum, m;
       attend_chunk<T, false, 64, false>(kimg, vimg, qf, wave, N, Npad, c2, lane, o, lsum, m, 0,
                                         -1, prio);
+      MICLIP_STAMP(1);   // the wave's full query chunk
       attend_store<T, 64>(o, lsum, wave, N, obase, D, lane);
+      MICLIP_STAMP(2);   // its output stores
     }
     if (nvalid > 0) {
       load_q<T, 64>(qf, base, ld, 8, N, lane);
@@ -531,8 +535,10 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
         }
       }
     }
+    MICLIP_STAMP(3);     // ragged chunk's key-tile slice + partial
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    MICLIP_STAMP(4);     // closing barrier
     // merge the ragged chunk: wave v takes queries v, v+8, ...; lane = output dim
     for (int c = wave; c < nvalid; c += 8) {
       const float* pc = part + (size_t)c * 66;
@@ -549,9 +555,11 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
       }
       obase[(size_t)(256 + c) * D + lane] = to_t<T>(acc / l);
     }
+    MICLIP_STAMP(5);     // merge
     // the merge's partial reads finish before the next head's partial writes:
     // those follow the next head's first barrier, which every merging wave joins
   }
+  MICLIP_STAMP_END(blockIdx.x * 8 + wave);
 }
 
 // MICLIP_ATTN=1 forces the one-head-per-workgroup kernel; 4 the pipelined

@@ -12,6 +12,46 @@
 
 #define MICLIP_DEV __device__ __forceinline__
 
+// In-kernel cycle stamps, compiled only into the diagnostic programs of
+// scripts/stamps/ (which define MICLIP_STAMPS before including a kernel source);
+// in the library every macro is empty. Per wave: the s_memtime cycles spent in
+// up to 8 segments (wave-uniform, SGPRs: s_memtime is a scalar READ), and at
+// exit lane 0 stores {segments, total cycles, s_memrealtime ticks (100 MHz)}
+// to miclip_stamp_buf[slot] with ordinary vector stores.
+#ifdef MICLIP_STAMPS
+constexpr int kStampWords = 10;
+extern __device__ unsigned long long miclip_stamp_buf[];
+struct StampAcc {
+  unsigned long long t, t0, r0, a0, a1, a2, a3, a4, a5, a6, a7;
+};
+#define MICLIP_STAMP_BEGIN                                                             \
+  StampAcc st_;                                                                        \
+  st_.r0 = __builtin_amdgcn_s_memrealtime();                                           \
+  st_.t = st_.t0 = __builtin_amdgcn_s_memtime();                                       \
+  st_.a0 = st_.a1 = st_.a2 = st_.a3 = st_.a4 = st_.a5 = st_.a6 = st_.a7 = 0
+#define MICLIP_STAMP(i)                                                                \
+  do {                                                                                 \
+    const unsigned long long n_ = __builtin_amdgcn_s_memtime();                        \
+    st_.a##i += n_ - st_.t;                                                            \
+    st_.t = n_;                                                                        \
+  } while (0)
+#define MICLIP_STAMP_END(slot)                                                         \
+  do {                                                                                 \
+    const unsigned long long e_ = __builtin_amdgcn_s_memtime();                        \
+    const unsigned long long r_ = __builtin_amdgcn_s_memrealtime();                    \
+    if ((threadIdx.x & 63) == 0) {                                                     \
+      unsigned long long* p_ = miclip_stamp_buf + (size_t)(slot) * kStampWords;        \
+      p_[0] = st_.a0; p_[1] = st_.a1; p_[2] = st_.a2; p_[3] = st_.a3;                  \
+      p_[4] = st_.a4; p_[5] = st_.a5; p_[6] = st_.a6; p_[7] = st_.a7;                  \
+      p_[8] = e_ - st_.t0; p_[9] = r_ - st_.r0;                                        \
+    }                                                                                  \
+  } while (0)
+#else
+#define MICLIP_STAMP_BEGIN
+#define MICLIP_STAMP(i)
+#define MICLIP_STAMP_END(slot)
+#endif
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -21,6 +61,7 @@ typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef short i16x8 __attribute__((ext_vector_type(8)));
 typedef short i16x4_vs __attribute__((__vector_size__(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 // Tiled MX scale planes (gemm_mx.hip): E8M0 byte of (row r, 32-k block kb) of an

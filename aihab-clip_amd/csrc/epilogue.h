@@ -136,6 +136,17 @@ struct EpiStore {
   }
   template <bool ASM = false>
   MICLIP_DEV void put4(int r, int c, float4 v, float4 b) const {
+    const i16x4 o = val4(v, b);
+    if constexpr (ASM)
+      st_b64_asm(C + (size_t)r * ldc + c, o);
+    else if (nt)
+      __builtin_nontemporal_store(o, (i16x4*)(C + (size_t)r * ldc + c));
+    else
+      *(i16x4*)(C + (size_t)r * ldc + c) = o;
+  }
+  // the 4 output elements of put4, returned instead of stored (the persistent
+  // kernel's transposed-accumulator epilogue stages them in LDS)
+  MICLIP_DEV i16x4 val4(float4 v, float4 b) const {
     i16x4 o;
     if constexpr (ACT == ACT_GELU || ACT == ACT_QUICKGELU) {  // packed-fp32 forms, same rounding
       const f32x2 y0 = (f32x2){v.x, v.y} + (f32x2){b.x, b.y};
@@ -156,12 +167,7 @@ struct EpiStore {
       o[2] = to_bits<T>(y1[0]);
       o[3] = to_bits<T>(y1[1]);
     }
-    if constexpr (ASM)
-      st_b64_asm(C + (size_t)r * ldc + c, o);
-    else if (nt)
-      __builtin_nontemporal_store(o, (i16x4*)(C + (size_t)r * ldc + c));
-    else
-      *(i16x4*)(C + (size_t)r * ldc + c) = o;
+    return o;
   }
   MICLIP_DEV void put1(int r, int c, float v, float b) const {
     C[(size_t)r * ldc + c] = to_t<T>(fin(act_fn<ACT>(v + b)));
@@ -207,6 +213,14 @@ struct EpiStoreLN {
   }
   template <bool ASM = false>
   MICLIP_DEV void put4ln(int r, int c, float4 v, float4 b, float4 s, float2 st) const {
+    const i16x4 o = val4ln(v, b, s, st);
+    if constexpr (ASM)
+      st_b64_asm(C + (size_t)r * ldc + c, o);
+    else
+      *(i16x4*)(C + (size_t)r * ldc + c) = o;
+  }
+  // put4ln's 4 output elements, returned instead of stored
+  MICLIP_DEV i16x4 val4ln(float4 v, float4 b, float4 s, float2 st) const {
     const f32x2 y0 = z2((f32x2){v.x, v.y}, (f32x2){s.x, s.y}, st, (f32x2){b.x, b.y});
     const f32x2 y1 = z2((f32x2){v.z, v.w}, (f32x2){s.z, s.w}, st, (f32x2){b.z, b.w});
     i16x4 o;
@@ -223,10 +237,7 @@ struct EpiStoreLN {
       o[2] = to_bits<T>(y1[0]);
       o[3] = to_bits<T>(y1[1]);
     }
-    if constexpr (ASM)
-      st_b64_asm(C + (size_t)r * ldc + c, o);
-    else
-      *(i16x4*)(C + (size_t)r * ldc + c) = o;
+    return o;
   }
   template <bool ASM = false>
   MICLIP_DEV void put4(int r, int c, float4 v, float4 b) const {
@@ -238,6 +249,12 @@ struct EpiStoreLN {
 };
 template <class Epi> struct IsLN : std::false_type {};
 template <typename T, int ACT> struct IsLN<EpiStoreLN<T, ACT>> : std::true_type {};
+// epilogues with a value form (val4 / val4ln): the persistent GEMM computes their
+// tiles with the MFMA operands swapped (a lane then holds 4 consecutive columns of
+// one row) and stages the converted outputs
+template <class Epi> struct TrAcc : std::false_type {};
+template <typename T, int ACT> struct TrAcc<EpiStoreLN<T, ACT>> : std::true_type {};
+template <typename T, int ACT> struct TrAcc<EpiStore<T, ACT>> : std::true_type {};
 
 // Residual stream X (R = float, or _Float16 as in the reference's fp16 GPU
 // model, clip/model.py:184-185 `x = x + ...` on half tensors) += acc + bias.

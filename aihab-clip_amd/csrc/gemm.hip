@@ -770,8 +770,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
 // tile; 0 for a partial tile, i.e. a full wait), never more than were issued.
 // The row tail runs at the end on the same workgroups (gemm_tail_wg tasks).
 // ---------------------------------------------------------------------------
-template <class Epi> struct EpiStores { static constexpr int n = 32; };   // 4 passes x 8 rows
-template <> struct EpiStores<EpiNull> { static constexpr int n = 0; };
+// global stores per lane of one tile's epilogue: 4 passes x 8 rows, or with
+// transposed accumulators 2 passes x 8 16-B stores
+template <class Epi, bool TR> struct EpiStores { static constexpr int n = TR ? 16 : 32; };
+template <bool TR> struct EpiStores<EpiNull, TR> { static constexpr int n = 0; };
 
 // {mean, rstd} of rows r0, r0+8, ..., r0+56 (wave-uniform r0, all in bounds) by
 // scalar loads: SGPR results, the lgkm counter only -- a vector load here would
@@ -805,24 +807,36 @@ MICLIP_DEV void wait_vmcnt_tile(int n) {
   switch (n) {
     case 36: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
     case 32: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+    case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
 
-template <typename T, class Epi>
+template <typename T, class Epi, bool TRQ = true>
 __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
                                                        const T* __restrict__ W, int M, int N,
                                                        int K, Epi epi, int gm, int ntm_dp,
                                                        int ntail, int tail_wide) {
+  // transposed accumulators (TrAcc epilogues): MFMA operands swapped, so each
+  // lane's accumulator holds 4 consecutive output columns of one output row
+  constexpr bool TR = TRQ && TrAcc<Epi>::value;
   constexpr int HALF = 128 * 128;        // bytes of one half-tile slot
   constexpr int EPI_LD = 260;            // fp32 row stride of the epilogue staging
   constexpr int STG = 4 * HALF;          // staging: 64 rows in the buffer-1 half onward
   constexpr int SMEM0 = 8 * HALF > STG + 64 * EPI_LD * 4 ? 8 * HALF : STG + 64 * EPI_LD * 4;
-  // folded LayerNorm (EpiStoreLN): the tile's column sums after the staging
-  constexpr int SMEM = SMEM0 + (IsLN<Epi>::value ? 256 * 4 : 0);
+  // TR staging: 128 rows of 256 outputs at a 520-B pitch (8-B skew per row); it
+  // fits where the fp32 staging sits
+  constexpr int TLD = 520;
+  static_assert(STG + 128 * TLD <= SMEM0, "TR staging");
+  // folded LayerNorm (EpiStoreLN): the tile's column sums after the staging; TR:
+  // the tile's bias and column sums [64] float4 and row statistics [256] float2
+  constexpr int SMEM = SMEM0 + (TR ? (IsLN<Epi>::value ? 4096 : 1024) : (IsLN<Epi>::value ? 1024 : 0));
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
   float4* lncs = (float4*)(smem + SMEM0);              // [64] column sums
+  float4* tbias = (float4*)(smem + SMEM0);             // TR: [64] bias
+  float4* tcs = (float4*)(smem + SMEM0 + 1024);        // TR LN: [64] column sums
+  float2* tst = (float2*)(smem + SMEM0 + 2048);        // TR LN: [256] {mean, rstd}
 
   const int ntn = N / 256, ntm = ntm_dp, ndp = ntm * ntn, nk = K / 64;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -886,13 +900,18 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[qi][qj][i][j] = Mfma<T>::m16(af[s][i], bf[s][j], acc[qi][qj][i][j]);
+        for (int j = 0; j < 2; ++j) {
+          if constexpr (TR)   // C^T = W . A^T: lane (fk, fr) = row fr, columns 4fk .. 4fk+3
+            acc[qi][qj][i][j] = Mfma<T>::m16(bf[s][j], af[s][i], acc[qi][qj][i][j]);
+          else
+            acc[qi][qj][i][j] = Mfma<T>::m16(af[s][i], bf[s][j], acc[qi][qj][i][j]);
+        }
     __builtin_amdgcn_s_setprio(0);
   };
 
   int prev_stores = -1;   // -1: first tile (full prologue)
   int id = blockIdx.x;
+  MICLIP_STAMP_BEGIN;
   if (id < ndp) sources(id, m0, n0, asrc, bsrc);
   for (; id < ndp; id += gridDim.x) {
 #pragma unroll
@@ -919,6 +938,7 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
     }
     lds_barrier();
     if (wr == 1) lds_barrier();   // stagger (wave-uniform)
+    MICLIP_STAMP(0);              // tile top: K-tile 0/1 staging and its wait
     for (int t = 0; t < nk; ++t) {
       const int buf = t & 1;
       const char* sA0 = smem + (buf * 4 + 0) * HALF + aoff;
@@ -953,6 +973,32 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
       }
     }
     if (wr == 0) lds_barrier();   // balance the stagger barrier
+    MICLIP_STAMP(1);              // main loop
+    if constexpr (TR) {
+      // the tile's epilogue operands, parked in LDS before the barrier below
+      // publishes them (their last readers, the previous tile's epilogue, are
+      // many barriers back); loaded and retired here, before anything else is
+      // in flight (a load left pending makes hipcc drain the prefetch later)
+      if (tid < 64) {
+        const float4 b = epi.bias4nb(n0 + tid * 4);
+        asm volatile("" ::"v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w));
+        tbias[tid] = b;
+      }
+      if constexpr (IsLN<Epi>::value) {
+        if (tid < 64) {
+          const float4 c = epi.colsum4nb(n0 + tid * 4);
+          asm volatile("" ::"v"(c.x), "v"(c.y), "v"(c.z), "v"(c.w));
+          tcs[tid] = c;
+        }
+        if (tid < 256) {
+          const int sr = m0 + tid;
+          const float2 st = epi.stats[sr < M ? sr : M - 1];
+          asm volatile("" ::"v"(st.x), "v"(st.y));
+          tst[tid] = st;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
 
     // ---- tile boundary: prefetch the next tile's K-tile 0 into buffer 0 ----
     lds_barrier();                 // every wave is done with both buffers
@@ -960,9 +1006,12 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
     // the bias is loaded and retired here, before anything is in flight: a
     // load left pending on some path makes hipcc wait vmcnt(0) at the next
     // tile's first MFMA that reuses its registers (draining the prefetch/stores)
-    const float4 bv = epi.bias4nb(cn0 + ec);   // branch-free (null bias -> zeros)
-    asm volatile("" ::"v"(bv.x), "v"(bv.y), "v"(bv.z), "v"(bv.w));
-    if constexpr (IsLN<Epi>::value) {
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (!TR) {
+      bv = epi.bias4nb(cn0 + ec);   // branch-free (null bias -> zeros)
+      asm volatile("" ::"v"(bv.x), "v"(bv.y), "v"(bv.z), "v"(bv.w));
+    }
+    if constexpr (IsLN<Epi>::value && !TR) {
       // the tile's column sums, retired here like the bias and parked in LDS
       // (read after the first pass's barrier). The row statistics are wave-
       // uniform per output row (a wave stores whole rows) and come in by
@@ -982,9 +1031,77 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
         glds16_hidden(src[1], dst + 1024);
       }
     }
+    const bool full = cm0 + 256 <= M;
+    MICLIP_STAMP(2);              // tile boundary: epilogue operands, prefetch issue
+    if constexpr (TR) {
+      // ---- transposed-accumulator epilogue: 2 passes of 128 rows (qi: tile rows
+      // wr*128 + qi*64 + 0..63). Every wave converts its own accumulators in
+      // registers (val4 / val4ln: put4's exact operations on 4 consecutive
+      // columns of one row) and writes the 8 output bytes with one ds_write_b64
+      // into a row-major image (pitch 520 B: the 16 rows of one write group land
+      // on 16 distinct 8-B bank slots); after the barrier each wave reads 16
+      // image rows back (ds_read_b64, 512 contiguous bytes per row) and stores
+      // them as 512-B row segments. fp16 staging: half the LDS bytes of the
+      // fp32 row staging, and no wave idles while another half stages.
+      char* img = smem + STG;
+#pragma unroll
+      for (int qi = 0; qi < 2; ++qi) {
+        if (qi > 0) lds_barrier();   // pass 0's readers are done with the image
+#pragma unroll
+        for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int c4 = wc * 16 + qj * 8 + j * 4 + fk;   // this lane's column quad
+            const float4 b = tbias[c4];
+            float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr (IsLN<Epi>::value) cs = tcs[c4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int ir = wr * 64 + i * 16 + fr;         // image row
+              const f32x4 a = acc[qi][qj][i][j];
+              const float4 v = make_float4(a[0], a[1], a[2], a[3]);
+              i16x4 o;
+              if constexpr (IsLN<Epi>::value)
+                o = epi.val4ln(v, b, cs, tst[wr * 128 + qi * 64 + i * 16 + fr]);
+              else
+                o = epi.val4(v, b);
+              *(i16x4*)(img + ir * TLD + (c4 & 1) * 256 + (c4 >> 1) * 8) = o;
+            }
+          }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        lds_barrier();
+        // readback: wave w stores image rows 16w .. 16w+15 in pairs (R, R+1). Lane
+        // (h, li) reads the 8 bytes at image half h of both rows (columns 8li + 4h
+        // .. +3); one v_permlane32_swap per dword then leaves lanes 0-31 with row R
+        // columns 8li .. 8li+7 and lanes 32-63 with row R+1 (guide T21): 16-B
+        // stores, each half-wave writing one whole 512-B row segment.
+        const int h = lane >> 5, li = lane & 31;
+        T* cb = epi.C + cn0 + li * 8;
+#pragma unroll
+        for (int p0 = 0; p0 < 8; p0 += 2) {
+          i16x4 va[2], vb[2];
+#pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            const int R = wave * 16 + 2 * (p0 + p);
+            va[p] = *(const i16x4*)(img + R * TLD + h * 256 + li * 8);
+            vb[p] = *(const i16x4*)(img + (R + 1) * TLD + h * 256 + li * 8);
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(va[0]), "+v"(va[1]), "+v"(vb[0]), "+v"(vb[1]));
+#pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            const u32x2 a = __builtin_bit_cast(u32x2, va[p]), b = __builtin_bit_cast(u32x2, vb[p]);
+            const auto s0 = __builtin_amdgcn_permlane32_swap(a[0], b[0], false, false);
+            const auto s1 = __builtin_amdgcn_permlane32_swap(a[1], b[1], false, false);
+            const u32x4 w = {s0[0], s1[0], s0[1], s1[1]};
+            const int ir = wave * 16 + 2 * (p0 + p) + h;
+            const int row = cm0 + (ir >> 6) * 128 + qi * 64 + (ir & 63);
+            if (full || row < M) *(u32x4*)(cb + (size_t)row * epi.ldc) = w;
+          }
+        }
+      }
+    } else {
     // ---- epilogue: 4 passes of 64 rows staged at STG ----
     float* stg = (float*)(smem + STG);
-    const bool full = cm0 + 256 <= M;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       if (p > 0) lds_barrier();
@@ -1094,8 +1211,10 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
         for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(xf[k]));
       }
     }
+    }
     lds_barrier();                 // staging (buffer-1 half) free for the next tile
-    prev_stores = full ? EpiStores<Epi>::n : 0;
+    prev_stores = full ? EpiStores<Epi, TR>::n : 0;
+    MICLIP_STAMP(3);              // epilogue
   }
   // the row tail on the same workgroups
   for (int task = blockIdx.x; task < ntail; task += gridDim.x) {
@@ -1105,6 +1224,8 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
     else
       gemm_tail_wg<T, Epi, 1, 64>(A, W, M, N, K, epi, ntm * 256, task, smem);
   }
+  MICLIP_STAMP(4);                // row tail
+  MICLIP_STAMP_END(blockIdx.x * 8 + wave);
 }
 
 // ---------------------------------------------------------------------------
@@ -1558,6 +1679,16 @@ int gemm_variant() {
   return v;
 }
 
+// Transposed-accumulator epilogue of the persistent kernel for EpiStore /
+// EpiStoreLN (MICLIP_GEMM_TRACC, default 1; 0 = the fp32 row staging, A/B)
+bool gemm_tracc() {
+  static bool v = [] {
+    const char* e = getenv("MICLIP_GEMM_TRACC");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 // Tile-row group of the 256x256 kernel's grouped order (MICLIP_GEMM_GROUP,
 // default 4; 1 = plain row-major). A variant >= 1000 carries it in its
 // thousands digit (diagnostic A/B through miclip_op_gemm).
@@ -1679,6 +1810,14 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
     const TailPlan tp = notail ? TailPlan{(M + 255) / 256, 0, 0} : plan_tail(M, N);
     const int ndp = tp.ntm_dp * (N / 256), ncu = cu_count();
     const int grid = ndp < ncu ? ndp : ncu;
+    if constexpr (TrAcc<Epi>::value) {
+      if (!gemm_tracc()) {
+        hipLaunchKernelGGL((gemm256s_kernel<T, Epi, false>), dim3(grid), dim3(512), 0, s,
+                           (const T*)A, (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs,
+                           tp.wide & 1);
+        return hipGetLastError();
+      }
+    }
     hipLaunchKernelGGL((gemm256s_kernel<T, Epi>), dim3(grid), dim3(512), 0, s, (const T*)A,
                        (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs, tp.wide & 1);
     return hipGetLastError();

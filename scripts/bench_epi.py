@@ -26,10 +26,11 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--shapes", default="qkv,fc,out,proj")
+    ap.add_argument("--m", type=int, default=256 * 257, help="rows (32896 = one splits=2 half)")
     args = ap.parse_args()
     lib = _lib.load_library()
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    M, W = 256 * 257, 1024
+    M, W = args.m, 1024
     g = torch.Generator(device="cuda").manual_seed(0)
     A = (torch.randn(M, 4 * W, device="cuda", generator=g) * 0.5).half()
     Wt = (torch.randn(4 * W, 4 * W, device="cuda", generator=g) * 0.02).half()
