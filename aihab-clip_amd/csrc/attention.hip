@@ -164,12 +164,17 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
     // Scalar f32 ops on purpose (this file builds with -fno-slp-vectorize):
     // beside MFMAs a v_pk_fma_f32 / v_pk_add_f32 issues slower than the two
     // scalar ops it replaces (MI355X_MICROARCH.md, per-instruction constants).
-    float ps[4] = {0.f, 0.f, 0.f, 0.f};
+    // (the partial sums start at the first four values: 0 + v == v for the
+    // non-negative exponentials, so this is the zero-initialised sum, 4 adds fewer)
+    float ps[4];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float v = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[r], c2, -m));
       sacc[r] = v;
-      ps[r & 3] += v;
+      if (r < 4)
+        ps[r] = v;
+      else
+        ps[r & 3] += v;
     }
     lsum += (ps[0] + ps[2]) + (ps[1] + ps[3]);   // the former packed pairs' order
     // ---- P^T as B operand: k-step s2 uses accumulator regs 8*s2 .. 8*s2+7 ----
@@ -223,18 +228,28 @@ MICLIP_DEV void attend_store(const f32x16 (&o)[HeadGeom<DH>::NDT], float lsum, i
   const int hh = lane >> 5;
   const int q = chunk * 32 + (lane & 31);
   const float inv = 1.0f / lsum;
-  if (q < N) {
-    T* op = op_row0 + (size_t)q * D;
+  // Lane (l32, hh) holds dims 8rg + 4hh .. +3 of query l32 for rg = 0..3 of each
+  // 32-dim tile. Per rg pair one v_permlane32_swap per dword (guide T21) leaves
+  // lane hh = 0 with dims 8rg .. 8rg+7 and lane hh = 1 with dims 8rg+8 .. 8rg+15:
+  // 16-B stores, half the store instructions. The swaps run on the full wave;
+  // the pair of lanes exchanging shares its query, hence the row guard.
+  T* op = op_row0 + (size_t)(q < N ? q : 0) * D;
 #pragma unroll
-    for (int dt = 0; dt < HeadGeom<DH>::NDT; ++dt) {
+  for (int dt = 0; dt < HeadGeom<DH>::NDT; ++dt) {
 #pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        if (32 * dt + 8 * rg >= DH) continue;  // padding dims (DH = 80: rg >= 2 of tile 2)
-        i16x4 w;
+    for (int rg = 0; rg < 4; rg += 2) {
+      if (32 * dt + 8 * rg >= DH) continue;  // padding dims (DH = 80: rg 2-3 of tile 2)
+      i16x4 w0, w1;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) w[e] = to_bits<T>(o[dt][4 * rg + e] * inv);
-        *(i16x4*)(op + 32 * dt + 8 * rg + 4 * hh) = w;
+      for (int e = 0; e < 4; ++e) {
+        w0[e] = to_bits<T>(o[dt][4 * rg + e] * inv);
+        w1[e] = to_bits<T>(o[dt][4 * rg + 4 + e] * inv);
       }
+      const u32x2 a = __builtin_bit_cast(u32x2, w0), b = __builtin_bit_cast(u32x2, w1);
+      const auto s0 = __builtin_amdgcn_permlane32_swap(a[0], b[0], false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(a[1], b[1], false, false);
+      const u32x4 v = {s0[0], s1[0], s0[1], s1[1]};
+      if (q < N) *(u32x4*)(op + 32 * dt + 8 * rg + 8 * hh) = v;
     }
   }
 }
