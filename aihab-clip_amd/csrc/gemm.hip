@@ -1763,11 +1763,17 @@ TailPlan plan_tail(int M, int N) {
   const int ntm_dp = ntm / step * step;
   const int rows = M - ntm_dp * 256;
   if (ntm_dp == 0 || rows <= 0 || rows > 256 || N % 64) return TailPlan{ntm, 0, 0};
-  // gemm_tail_wg tasks: 32 x 128 when that still gives >= ncu/2 workgroups
-  // (less W re-read per row), else 16 x 64
+  // gemm_tail_wg tasks: 32 x 128 or 16 x 64, whichever ends sooner: the tail
+  // adds (tasks per workgroup) x (task time) to the launch, and a wide task
+  // takes ~1.5x a narrow one (in-kernel stamps, K = 1024: 19.6k vs 12.8k cycles;
+  // ViT-L/14 QKV at M = 32896: 384 narrow tasks = 2 per workgroup -> 96 wide
+  // ones, the tail's share of the launch 5.2 -> 2.1 %)
   const int wide_tasks = (rows + 31) / 32 * (N / 128);
-  if (N % 128 == 0 && 2 * wide_tasks >= ncu) return TailPlan{ntm_dp, wide_tasks, 1};
-  return TailPlan{ntm_dp, (rows + 15) / 16 * (N / 64), 0};
+  const int narrow_tasks = (rows + 15) / 16 * (N / 64);
+  const int wide_cost = (wide_tasks + ncu - 1) / ncu * 3;
+  const int narrow_cost = (narrow_tasks + ncu - 1) / ncu * 2;
+  if (N % 128 == 0 && wide_cost < narrow_cost) return TailPlan{ntm_dp, wide_tasks, 1};
+  return TailPlan{ntm_dp, narrow_tasks, 0};
 }
 
 bool gemm_shape_ok(int M, int N, int K) {
