@@ -691,6 +691,17 @@ int miclip_reserve(miclip_model* m, int32_t max_images, int32_t max_prompts) {
   return 0;
 }
 
+// Parts the batch of B images (N tokens each) is split into over streams: at
+// most m->splits, no part below 16 images, and none below kSplitRows rows -- a
+// part must keep its GEMMs above about one round of 256x256 tiles (ViT-B/32
+// bs=256, 12 800 rows: 71.0k img/s unsplit vs 64.8k split in two, same process).
+static int image_splits(const miclip_model* m, int B, int N) {
+  constexpr int64_t kSplitRows = 16384;
+  int splits = m->profiling ? 1 : m->splits;
+  while (splits > 1 && (B < 16 * splits || (int64_t)B * N < kSplitRows * splits)) --splits;
+  return splits;
+}
+
 int miclip_encode_image(miclip_model* m, const float* images, int32_t B, float* out,
                         uint32_t flags, void* stream) {
   if (!m || !images || !out || B < 1) return fail(MICLIP_EINVAL, "bad argument to encode_image");
@@ -709,8 +720,7 @@ int miclip_encode_image(miclip_model* m, const float* images, int32_t B, float* 
   // part's HBM-bound epilogues / LayerNorm / attention run beside another part's
   // MFMA-bound GEMMs, and a GEMM's partial last wave of tiles is filled by
   // another stream's work). Each part uses its own window of the workspace.
-  int splits = m->profiling ? 1 : m->splits;
-  while (splits > 1 && B < 16 * splits) --splits;
+  const int splits = image_splits(m, B, N);
   if (splits == 1) return encode_image_part(m, view(m, m->wimg, 0, 0, N, W), images, B, out, flags, s);
   if ((rc = ensure_aux(m, splits - 1))) return rc;
   MICLIP_HIP(hipEventRecord(m->ev_fork, s));
@@ -730,6 +740,12 @@ int miclip_encode_image(miclip_model* m, const float* images, int32_t B, float* 
     MICLIP_HIP(hipStreamWaitEvent(s, m->ev_join[p - 1], 0));
   }
   return 0;
+}
+
+int miclip_image_splits(const miclip_model* m, int32_t B) {
+  if (!m || B < 1) return fail(MICLIP_EINVAL, "bad argument to image_splits");
+  const int g = m->cfg.image_resolution / m->cfg.vision_patch_size;
+  return image_splits(m, B, g * g + 1);
 }
 
 int miclip_set_splits(miclip_model* m, int32_t splits) {

@@ -10,7 +10,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MICLIP_LIB", os.path.join(_HERE, "libmiclip.so"))
 
-ABI_VERSION = 4          # include/miclip.h MICLIP_ABI_VERSION
+ABI_VERSION = 5          # include/miclip.h MICLIP_ABI_VERSION
 MICLIP_FP16 = 0
 MICLIP_BF16 = 1
 MICLIP_MXFP8 = 2
@@ -27,7 +27,7 @@ EXPORTS = (
     "miclip_reserve",
     "miclip_encode_image", "miclip_encode_text", "miclip_zero_shot",
     "miclip_model_destroy", "miclip_last_error", "miclip_abi_version",
-    "miclip_model_bytes", "miclip_model_flags", "miclip_set_profiling", "miclip_profile_read", "miclip_set_splits",
+    "miclip_model_bytes", "miclip_model_flags", "miclip_set_profiling", "miclip_profile_read", "miclip_set_splits", "miclip_image_splits",
     "miclip_op_gemm", "miclip_op_ln_stats", "miclip_op_ln_fold", "miclip_op_gemm_ln",
     "miclip_op_layernorm", "miclip_op_attention", "miclip_preprocess",
     "miclip_row_norms", "miclip_class_centroids", "miclip_proto_scores",
@@ -93,6 +93,7 @@ def load_library(path: str = None):
         "miclip_model_flags": ([vp], ctypes.c_int),
         "miclip_set_profiling": ([vp, ctypes.c_int], ctypes.c_int),
         "miclip_set_splits": ([vp, i32], ctypes.c_int),
+        "miclip_image_splits": ([vp, i32], ctypes.c_int),
         "miclip_profile_read": ([vp, ctypes.POINTER(MiclipKernelStat), i32, i32], ctypes.c_int),
         "miclip_op_gemm": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp], ctypes.c_int),
         "miclip_op_layernorm": ([i32, vp, vp, vp, vp, i32, i32, i32, vp], ctypes.c_int),

@@ -184,6 +184,13 @@ class CLIP(nn.Module):
         h = self._require()
         _lib.check(h.lib.miclip_set_splits(h.ptr, int(splits)), "miclip_set_splits")
 
+    def image_splits(self, batch):
+        """Parts encode_image splits `batch` images into (miclip_image_splits)."""
+        h = self._require()
+        n = h.lib.miclip_image_splits(h.ptr, int(batch))
+        _lib.check(0 if n > 0 else n, "miclip_image_splits")
+        return n
+
     def numerics(self):
         """The handle's numerics path: dict(resid16, lnfold, mxfp8) (miclip_model_flags)."""
         h = self._require()

@@ -268,8 +268,10 @@ def run(args):
         ab = {}
         for sp in (1, 2, 3, 1, 2, 3):
             model.set_splits(sp)
+            eff = model.image_splits(max(hi - lo, 1))   # the part count actually run
             step()
-            ab.setdefault(f"splits{sp}", []).append(round(n_global * args.steps / timed(step, args.steps), 1))
+            ab.setdefault(f"splits{sp}" + (f"_ran{eff}" if eff != sp else ""), []).append(
+                round(n_global * args.steps / timed(step, args.steps), 1))
         model.set_splits(args.splits)
     abf = None
     if args.ab_fold:
@@ -345,7 +347,8 @@ def run(args):
                        "global_batch": n_global, "images_per_gpu": hi - lo,
                        "tokens_per_image": cfg.n_tokens,
                        "parallelism": f"dp{world} (image-batch sharding, {args.scaling} scaling)",
-                       "splits": args.splits, "numerics": model.numerics(),
+                       "splits": model.image_splits(max(hi - lo, 1)),
+                       "splits_requested": args.splits, "numerics": model.numerics(),
                        "weights": "seeded random init, CLIP shapes"},
             "gflop_per_image": round(gf, 3),
             "path_mfma_frac": round(value * gf * 1e9 / (world * peak * 1e12), 4),

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MICLIP_ABI_VERSION 4
+#define MICLIP_ABI_VERSION 5
 
 enum miclip_status {
   MICLIP_OK = 0,
@@ -176,6 +176,9 @@ int miclip_proto_scores(const float* x, const float* protos, const int32_t* owne
  * graph-capturable): 1 = off, 2..4 = that many parts (default 2; a part is
  * never smaller than 16 images). */
 int miclip_set_splits(miclip_model* m, int32_t splits);
+/* Parts encode_image splits a batch of B images into (>= 1): at most the
+ * miclip_set_splits value, no part below 16 images or 16384 token rows. */
+int miclip_image_splits(const miclip_model* m, int32_t B);
 
 void miclip_model_destroy(miclip_model* m);
 const char* miclip_last_error(void);

@@ -229,6 +229,7 @@ def test_benched_config_vitl14_bs256(golden):
     batch[rows] = gold
     _, m, _ = miclip.load("ViT-L/14", device="cuda", compute_dtype="fp16")
     m.set_splits(2)
+    assert m.image_splits(256) == 2 and m.image_splits(4) == 1
     feats = m.encode_image(torch.from_numpy(batch).cuda()).cpu()
     d = _one_minus_cos(feats[rows], g["image"])
     print(f"bs=256 golden rows 1-cos {d}")

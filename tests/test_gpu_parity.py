@@ -139,6 +139,10 @@ def test_batch_invariance_and_shards():
     exactly the single-GPU cache."""
     from miclip.weights import synthetic_images
     m = _model("ViT-B/32", "fp16")
+    # 96 x 50 token rows: below the split threshold, one stream (the split path
+    # at the benched batch: test_gpu_lnfold.test_benched_config_vitl14_bs256)
+    assert m.image_splits(96) == 1 and m.image_splits(256) == 1
+    m.set_splits(2)
     imgs = torch.from_numpy(synthetic_images(96, 224, seed=3)).cuda()
     full = m.encode_image(imgs)
     parts = torch.cat([m.encode_image(imgs[i:i + 32]) for i in range(0, 96, 32)])
