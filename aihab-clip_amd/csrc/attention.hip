@@ -577,6 +577,115 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
   MICLIP_STAMP_END(blockIdx.x * 8 + wave);
 }
 
+// ---------------------------------------------------------------------------
+// One query per (image, head): token row 0 (CLS) only. The vision tower's last
+// block feeds nothing but the CLS rows forward (VisionTransformer.forward,
+// clip/model.py:226-229: ln_post(x[:, 0, :])), so there the attention of the
+// other N-1 queries is dead work. One wave per (image, head), four per
+// workgroup, all on VALU (1 x N x dh MACs per head; the K / V rows stream from
+// the QKV buffer). Lane l scores keys l, l+64, ... with v_dot2c_f32_{f16,bf16}
+// (fp32 sums of the exact fp16 products), exponentials in base 2 relative to
+// the row max, P rounded to the compute dtype for P.V as in the MFMA kernels
+// (whose B operand it is there), P.V accumulated in fp32 with lane = output
+// dim pair; out: compact [B, H*dh] (row b = image b's CLS row).
+// ---------------------------------------------------------------------------
+template <typename T>
+MICLIP_DEV float dot2acc(uint32_t a, uint32_t b, float c);
+template <>
+MICLIP_DEV float dot2acc<_Float16>(uint32_t a, uint32_t b, float c) {
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  return __builtin_amdgcn_fdot2(__builtin_bit_cast(h2, a), __builtin_bit_cast(h2, b), c, false);
+}
+template <>
+MICLIP_DEV float dot2acc<__bf16>(uint32_t a, uint32_t b, float c) {
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(b2, a), __builtin_bit_cast(b2, b), c,
+                                         false);
+}
+
+constexpr int kQ0MaxN = 640;   // keys per head (10 per lane)
+
+template <typename T, int DH>
+__global__ __launch_bounds__(256) void attention_q0_kernel(const T* __restrict__ qkv,
+                                                           T* __restrict__ out, int B, int N,
+                                                           int H, float c2) {
+  constexpr int NV = DH / 8;          // 16-B vectors per row
+  constexpr int NP = DH / 2;          // output dim pairs
+  constexpr int KPI = 64 / NP;        // keys per P.V step (2 for dh 64, 1 for dh 80)
+  constexpr int NJ = kQ0MaxN / 64;    // key passes
+  const int lane = threadIdx.x & 63;
+  const int bh = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (bh >= B * H) return;            // whole wave
+  const int b = bh / H, h = bh - b * H;
+  const int D = H * DH, ld = 3 * D;
+  const T* base = qkv + (size_t)b * N * ld + h * DH;
+  u32x4 qv[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) qv[i] = *(const u32x4*)(base + 8 * i);
+  float sc[NJ];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int k = lane + 64 * j;
+    float a = -INFINITY;
+    if (64 * j < N) {                 // wave-uniform pass guard
+      const T* kr = base + (size_t)(k < N ? k : N - 1) * ld + D;
+      u32x4 kv[NV];
+#pragma unroll
+      for (int i = 0; i < NV; ++i) kv[i] = *(const u32x4*)(kr + 8 * i);
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = dot2acc<T>(qv[i][e], kv[i][e], acc);
+      a = k < N ? acc * c2 : -INFINITY;
+    }
+    sc[j] = a;
+    mx = fmaxf(mx, a);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  float lsum = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const float pj = __builtin_amdgcn_exp2f(sc[j] - mx);   // exp2(-inf) = 0 past N
+    sc[j] = pj;
+    lsum += pj;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) lsum += __shfl_xor(lsum, o);
+  // P.V: lane (sub, dp) = key parity sub, output dims 2dp, 2dp+1
+  const int sub = lane / NP, dp = lane - sub * NP;
+  const bool act = sub < KPI;
+  float a0 = 0.f, a1 = 0.f;
+  const T* vb = base + 2 * D + 2 * dp;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    if (64 * j >= N) break;           // wave-uniform
+    for (int kk = 0; kk < 64; kk += KPI) {
+      const int src = kk + (act ? sub : 0);
+      const float pk = __shfl(sc[j], src);
+      const int k = 64 * j + src;
+      if (act && k < N) {
+        const uint32_t v = *(const uint32_t*)(vb + (size_t)k * ld);
+        const float p16 = to_f<T>(to_t<T>(pk));
+        a0 = __builtin_fmaf(p16, from_bits<T>((short)(v & 0xffff)), a0);
+        a1 = __builtin_fmaf(p16, from_bits<T>((short)(v >> 16)), a1);
+      }
+    }
+  }
+  if constexpr (KPI == 2) {           // the two key parities' partial sums
+    a0 += __shfl_xor(a0, 32);
+    a1 += __shfl_xor(a1, 32);
+  }
+  if (lane < NP) {
+    const float inv = 1.0f / lsum;
+    const uint32_t w = (uint32_t)(uint16_t)to_bits<T>(a0 * inv) |
+                       ((uint32_t)(uint16_t)to_bits<T>(a1 * inv) << 16);
+    *(uint32_t*)(out + (size_t)b * D + h * DH + 2 * dp) = w;
+  }
+}
+
 // MICLIP_ATTN=1 forces the one-head-per-workgroup kernel; 4 the pipelined
 // kernel with the last-chunk split (A/B comparisons).
 int attn_variant() {
@@ -718,6 +827,31 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, 
 }
 
 }  // namespace
+
+hipError_t attention_q0(int dtype, const void* qkv, void* out, int B, int N, int H,
+                        hipStream_t s, int head_dim) {
+  if (B < 1 || N < 1 || H < 1 || N > kQ0MaxN) return hipErrorInvalidValue;
+  if (head_dim == 0) head_dim = 64;
+  if (head_dim != 64 && head_dim != 80) return hipErrorInvalidValue;
+  const int grid = (B * H + 3) / 4;
+  const float c2 = kLog2e / sqrtf((float)head_dim);
+  if (dtype == kF16) {
+    if (head_dim == 64)
+      hipLaunchKernelGGL((attention_q0_kernel<_Float16, 64>), dim3(grid), dim3(256), 0, s,
+                         (const _Float16*)qkv, (_Float16*)out, B, N, H, c2);
+    else
+      hipLaunchKernelGGL((attention_q0_kernel<_Float16, 80>), dim3(grid), dim3(256), 0, s,
+                         (const _Float16*)qkv, (_Float16*)out, B, N, H, c2);
+  } else {
+    if (head_dim == 64)
+      hipLaunchKernelGGL((attention_q0_kernel<__bf16, 64>), dim3(grid), dim3(256), 0, s,
+                         (const __bf16*)qkv, (__bf16*)out, B, N, H, c2);
+    else
+      hipLaunchKernelGGL((attention_q0_kernel<__bf16, 80>), dim3(grid), dim3(256), 0, s,
+                         (const __bf16*)qkv, (__bf16*)out, B, N, H, c2);
+  }
+  return hipGetLastError();
+}
 
 hipError_t attention(int dtype, const void* qkv, void* out, int B, int N, int H, int causal,
                      hipStream_t s, int variant, int head_dim) {

@@ -96,6 +96,7 @@ struct Workspace {
   void* f = nullptr;
   // MX-fp8 models: LayerNorm output (hq, scales hs) and c_fc output (fq, fs)
   void *hq = nullptr, *hs = nullptr, *fq = nullptr, *fs = nullptr;
+  void* xc = nullptr;     // [items, W] the CLS rows of x (last vision block, run_block)
   float* feat = nullptr;  // [items, W] fp32 scratch
   int32_t* rows = nullptr;
   float* stats = nullptr;  // [rows] {mean, rstd} for the folded LayerNorm
@@ -165,13 +166,15 @@ struct miclip_model {
 
 namespace {
 
+// K_CLS_BLOCK: everything of the last vision block after its QKV GEMM, on the
+// CLS rows only (run_block cls_only)
 enum KClass {
   K_IM2COL, K_GEMM_PATCH, K_LAYERNORM, K_GEMM_QKV, K_ATTENTION, K_GEMM_OUT, K_GEMM_FC,
-  K_GEMM_PROJ, K_HEAD, K_TEXT_EMBED, K_NUM
+  K_GEMM_PROJ, K_HEAD, K_TEXT_EMBED, K_CLS_BLOCK, K_NUM
 };
 const char* const kClassNames[K_NUM] = {"im2col", "gemm_patch", "layernorm", "gemm_qkv",
                                         "attention", "gemm_out", "gemm_fc", "gemm_proj",
-                                        "head", "text_embed"};
+                                        "head", "text_embed", "cls_block"};
 
 hipEvent_t take_event(miclip_model* m) {
   if (!m->event_pool.empty()) {
@@ -266,7 +269,7 @@ int ensure_ws(miclip_model* m, Workspace& w, int items, int ntok, int W, bool im
   const size_t e = elt();
   // grow: make sure no queued kernel still uses the old buffers
   MICLIP_HIP(hipDeviceSynchronize());
-  for (void* p : {w.patches, (void*)w.x, w.h, w.qkv, w.o, w.f, w.hq, w.hs, w.fq, w.fs,
+  for (void* p : {w.patches, (void*)w.x, w.h, w.qkv, w.o, w.f, w.hq, w.hs, w.fq, w.fs, w.xc,
                   (void*)w.feat, (void*)w.rows, (void*)w.stats})
     dev_free(m, p);
   w = Workspace{};
@@ -289,6 +292,7 @@ int ensure_ws(miclip_model* m, Workspace& w, int items, int ntok, int W, bool im
     if ((rc = dev_alloc(m, &w.fq, (size_t)rows * 4 * W))) return rc;
     if ((rc = dev_alloc(m, &w.fs, mx_scale_bytes(rows + 4 * 256, 4 * W)))) return rc;
   }
+  if ((rc = dev_alloc(m, &w.xc, (size_t)items * W * (m->resid16 ? 2 : 4)))) return rc;
   if ((rc = dev_alloc(m, (void**)&w.feat, (size_t)items * W * 4))) return rc;
   if ((rc = dev_alloc(m, (void**)&w.rows, (size_t)items * 4))) return rc;
   if ((rc = dev_alloc(m, (void**)&w.stats, (size_t)rows * 8))) return rc;
@@ -330,8 +334,17 @@ int ensure_folded(miclip_model* m, bool visual) {
   return 0;
 }
 
+// One ResidualAttentionBlock (clip/model.py:183-186) over items x N token rows.
+// cls_only (the vision tower's last block): VisionTransformer.forward keeps only
+// ln_post(x[:, 0, :]) of its output (clip/model.py:226-229), so after the QKV
+// GEMM over all rows (every token's key and value) only the CLS query is
+// attended (attention_q0) and out-proj, ln_2 and the MLP run on the items CLS
+// rows, gathered into the compact residual block w.xc. Row for row these are the
+// same operations as the full block (GEMM rows are independent; the tile and row-
+// tail paths round alike), so the CLS features are those of the full block up to
+// the attention's summation order.
 int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, int W, int H,
-              int dh, int causal, hipStream_t s) {
+              int dh, int causal, hipStream_t s, bool cls_only = false) {
   const int M = items * N, dt = m->dtype, r16 = m->resid16;
   const double dM = M, dW = W, rb = r16 ? 2 : 4;  // residual bytes per element
   const bool mx = m->mx;   // MX-fp8 operands for QKV / c_fc / c_proj
@@ -358,6 +371,27 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
                                ACT_NONE, s));
     else
       MICLIP_HIP(gemm_store(dt, w.h, b.w_qkv, b.b_qkv, w.qkv, M, 3 * W, W, ACT_NONE, s));
+  }
+  if (cls_only) {
+    const double dI = items;
+    ProfScope p(m, K_CLS_BLOCK, s,
+                4.0 * dI * H * N * dh + gemm_flops(dI, dW, dW) + gemm_flops(dI, 4 * dW, dW) +
+                    gemm_flops(dI, dW, 4 * dW),
+                dM * 2 * dW * 2 + 10 * dW * dW * 2);
+    MICLIP_HIP(attention_q0(dt, w.qkv, w.o, items, N, H, s, dh));
+    MICLIP_HIP(gather_rows(w.x, w.xc, items, N, W, r16 ? 2 : 4, s));
+    MICLIP_HIP(gemm_residual(dt, w.o, b.w_out, b.b_out, w.xc, items, W, W, s, 0, r16));
+    if (fold) {
+      MICLIP_HIP(ln_stats(w.xc, w.stats, items, W, s, b.fs_fc));
+      MICLIP_HIP(gemm_store_ln(dt, w.xc, b.wf_fc, b.c_fc, b.cs_fc, w.stats, w.f, items, 4 * W, W,
+                               m->cfg.act, s));
+    } else {
+      MICLIP_HIP(
+          layernorm(dt, w.xc, nullptr, 1, b.ln2_g, b.ln2_b, nullptr, w.h, items, W, 0, s, r16));
+      MICLIP_HIP(gemm_store(dt, w.h, b.w_fc, b.b_fc, w.f, items, 4 * W, W, m->cfg.act, s));
+    }
+    MICLIP_HIP(gemm_residual(dt, w.f, b.w_proj, b.b_proj, w.xc, items, W, 4 * W, s, 0, r16));
+    return 0;
   }
   {
     const double n = N;
@@ -426,6 +460,7 @@ Workspace view(const miclip_model* m, const Workspace& w, size_t row0, size_t it
     v.hs = (char*)w.hs + blk * (W / 128) * 1024;
     v.fs = (char*)w.fs + blk * (4 * W / 128) * 1024;
   }
+  v.xc = (char*)w.xc + item0 * W * (m->resid16 ? 2 : 4);
   v.feat = w.feat + item0 * W;
   v.rows = w.rows + item0;
   v.stats = w.stats + 2 * row0;
@@ -440,6 +475,13 @@ int ensure_aux(miclip_model* m, int n) {
     if (!m->ev_join[i]) MICLIP_HIP(hipEventCreateWithFlags(&m->ev_join[i], hipEventDisableTiming));
   }
   return 0;
+}
+
+// MICLIP_CLS_LAST=0 runs the vision tower's last block over every row (A/B,
+// tests); default 1: CLS rows only (run_block cls_only)
+bool cls_last_block() {
+  const char* e = getenv("MICLIP_CLS_LAST");   // read per encode call (tests switch it)
+  return !e || atoi(e) != 0;
 }
 
 // encode_image for B images whose workspace window is `w` (clip/model.py:216-235)
@@ -471,17 +513,25 @@ int encode_image_part(miclip_model* m, Workspace w, const float* images, int B, 
                          m->resid16 ? nullptr : (float*)w.x, m->resid16 ? w.x : nullptr, M, W,
                          0, s, m->resid16));
   }
+  // the last block on the CLS rows only (run_block); MX-fp8 models and (never
+  // for CLIP's towers) N beyond attention_q0's range run it whole
+  const bool cls_last = cls_last_block() && !m->mx && N <= 640;
   for (int l = 0; l < c.vision_layers; ++l)
-    if ((rc = run_block(m, m->vblocks[l], w, B, N, W, H, dh, 0, s))) return rc;
+    if ((rc = run_block(m, m->vblocks[l], w, B, N, W, H, dh, 0, s,
+                        cls_last && l == c.vision_layers - 1)))
+      return rc;
   const bool proj = flags & MICLIP_FLAG_APPLY_PROJ, norm = flags & MICLIP_FLAG_NORMALIZE;
-  // ln_post on the CLS rows only (clip/model.py:228): rows b*N
+  // ln_post on the CLS rows only (clip/model.py:228): rows b*N of x, or the
+  // compact CLS block xc
+  const void* xcls = cls_last ? w.xc : w.x;
+  const int cstride = cls_last ? 1 : N;
   ProfScope p(m, K_HEAD, s, proj ? 2.0 * B * W * c.embed_dim : 0.0, (double)B * W * 8);
   if (!proj) {
-    MICLIP_HIP(layernorm(dt, w.x, nullptr, N, m->ln_post_g, m->ln_post_b, out, nullptr, B, W,
-                         norm ? 1 : 0, s, m->resid16));
+    MICLIP_HIP(layernorm(dt, xcls, nullptr, cstride, m->ln_post_g, m->ln_post_b, out, nullptr, B,
+                         W, norm ? 1 : 0, s, m->resid16));
   } else {
-    MICLIP_HIP(layernorm(dt, w.x, nullptr, N, m->ln_post_g, m->ln_post_b, w.feat, nullptr, B, W,
-                         0, s, m->resid16));
+    MICLIP_HIP(layernorm(dt, xcls, nullptr, cstride, m->ln_post_g, m->ln_post_b, w.feat, nullptr,
+                         B, W, 0, s, m->resid16));
     MICLIP_HIP(rowvec_matmul(w.feat, m->vproj, out, B, W, c.embed_dim, s));
     if (norm) MICLIP_HIP(row_l2norm(out, B, c.embed_dim, s));
   }
@@ -976,6 +1026,14 @@ int miclip_op_attention(int32_t dtype, const void* qkv, void* out, int32_t B, in
 
 int64_t miclip_mx_scale_bytes(int32_t rows, int32_t K) {
   return rows < 1 || K < 128 ? 0 : (int64_t)mx_scale_bytes(rows, K);
+}
+
+int miclip_op_attention_q0(int32_t dtype, const void* qkv, void* out, int32_t B, int32_t N,
+                           int32_t H, int32_t head_dim, void* stream) {
+  if (!qkv || !out) return fail(MICLIP_EINVAL, "null pointer");
+  if (dtype != MICLIP_FP16 && dtype != MICLIP_BF16) return fail(MICLIP_EINVAL, "bad dtype");
+  MICLIP_HIP(attention_q0(dtype, qkv, out, B, N, H, (hipStream_t)stream, head_dim));
+  return 0;
 }
 
 int miclip_op_quant_mx(const void* in, int32_t in_f16, int32_t R, int32_t K, void* q, void* scales,

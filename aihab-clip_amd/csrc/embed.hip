@@ -245,6 +245,17 @@ __global__ __launch_bounds__(64) void row_l2norm_kernel(float* __restrict__ x, i
   for (int d = threadIdx.x; d < D; d += 64) row[d] *= inv;
 }
 
+// dst row r = src row r * stride_rows, 16-B chunks (the CLS rows of the residual
+// stream for the last vision block, capi.hip run_block_cls)
+__global__ void gather_rows_kernel(const char* __restrict__ src, char* __restrict__ dst,
+                                   int stride_rows, int row_bytes) {
+  const int r = blockIdx.x;
+  const char* sp = src + (size_t)r * stride_rows * row_bytes;
+  char* dp = dst + (size_t)r * row_bytes;
+  for (int c = threadIdx.x * 16; c < row_bytes; c += blockDim.x * 16)
+    *(u32x4*)(dp + c) = *(const u32x4*)(sp + c);
+}
+
 }  // namespace
 
 // Weight repack at load (convert_weights, clip/model.py:372-393): fp32 rows
@@ -260,6 +271,16 @@ __global__ __launch_bounds__(256) void cast_pad_kernel(const float* __restrict__
     const int c = (int)(i - r * cols);
     out[i] = (T)(c < src_cols ? in[r * src_cols + c] : 0.f);
   }
+}
+
+hipError_t gather_rows(const void* src, void* dst, int R, int stride_rows, int D, int elt_bytes,
+                       hipStream_t s) {
+  const int row_bytes = D * elt_bytes;
+  if (R < 1 || stride_rows < 1 || row_bytes % 16 || (elt_bytes != 2 && elt_bytes != 4))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(R), dim3(256), 0, s, (const char*)src, (char*)dst,
+                     stride_rows, row_bytes);
+  return hipGetLastError();
 }
 
 hipError_t cast_pad(int dtype, const float* in, void* out, int64_t rows, int src_cols, int cols,

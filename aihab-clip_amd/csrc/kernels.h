@@ -87,7 +87,15 @@ hipError_t ln_fold(int dtype, const void* W, const float* gamma, const float* be
 hipError_t attention(int dtype, const void* qkv, void* out, int B, int N, int H, int causal,
                      hipStream_t s, int variant = 0, int head_dim = 64);
 
+// Attention of token row 0 (CLS) of every image only: out [B, H*dh] compact
+// (row b = image b's CLS row), same qkv layout; N <= 640, dh 64 or 80 (0 = 64).
+hipError_t attention_q0(int dtype, const void* qkv, void* out, int B, int N, int H,
+                        hipStream_t s, int head_dim = 64);
+
 // ---- embeddings / gathers ----
+// dst[r, :] = src[r * stride_rows, :], rows of D elements of elt_bytes (2 or 4)
+hipError_t gather_rows(const void* src, void* dst, int R, int stride_rows, int D, int elt_bytes,
+                       hipStream_t s);
 // images fp32 [B,3,R,R] -> patches [B*g*g, Kp] compute dtype, col = c*P*P + ky*P + kx,
 // zero-padded up to Kp (multiple of 64).
 hipError_t im2col(int dtype, const float* img, void* patches, int B, int R, int P, int Kp,

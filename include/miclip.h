@@ -265,6 +265,13 @@ int miclip_op_attention(int32_t dtype, const void* qkv, void* out, int32_t B, in
                         int32_t H, int32_t head_dim, int32_t causal, int32_t variant,
                         void* stream);
 
+/* Attention of the first query (token row 0, CLS) of every image only, same qkv
+ * layout as miclip_op_attention; out [B, H*dh] compact (row b = image b's CLS
+ * row). The vision tower's last block (only its CLS rows reach ln_post,
+ * clip/model.py:226-229). N <= 640, dh 64 or 80 (0 = 64), non-causal. */
+int miclip_op_attention_q0(int32_t dtype, const void* qkv, void* out, int32_t B, int32_t N,
+                           int32_t H, int32_t head_dim, void* stream);
+
 /* ---- MX-fp8 operands (MICLIP_MXFP8; no reference counterpart: C5 stretch) ----
  * An MX-fp8 [rows, K] operand is e4m3 bytes [rows, K] plus a tiled E8M0 scale
  * plane of miclip_mx_scale_bytes(rows, K) bytes (one scale per 32 consecutive k). */

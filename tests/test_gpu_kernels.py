@@ -280,6 +280,31 @@ def test_attention_dh80(lib, dt, B, N, H, causal):
     assert bool((out[B * N] == 7.0).all())
 
 
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+@pytest.mark.parametrize("B,N,H,dh", [(3, 257, 16, 64), (2, 577, 16, 64), (5, 50, 12, 64),
+                                      (2, 257, 16, 80), (1, 1, 1, 64), (2, 640, 2, 64),
+                                      (7, 197, 3, 64), (1, 65, 5, 80)])
+def test_attention_q0(lib, dt, B, N, H, dh):
+    """CLS-query attention (the vision tower's last block): row 0 of each image
+    against fp32 SDPA, compact [B, H*dh] output; rows past B untouched."""
+    code, tdt = DT[dt]
+    g = torch.Generator(device="cuda").manual_seed(B * 1000 + N + H + dh)
+    qkv = (torch.randn(B * N, 3 * H * dh, device="cuda", generator=g) * 1.5).to(tdt)
+    out = torch.full((B + 1, H * dh), 7.0, device="cuda", dtype=tdt)
+    _check(lib, lib.miclip_op_attention_q0(code, qkv.data_ptr(), out.data_ptr(), B, N, H, dh,
+                                           _stream()))
+    torch.cuda.synchronize()
+    ref = _attn_ref(qkv, B, N, H, 0, dh=dh).view(B, N, H * dh)[:, 0]
+    err = (out[:B].float() - ref).abs().max().item()
+    assert err < (4e-2 if dt == "bf16" else 6e-3), err
+    assert bool((out[B] == 7.0).all())
+    # out of range: N beyond the kernel's key capacity, head dims other than 64 / 80
+    assert lib.miclip_op_attention_q0(code, qkv.data_ptr(), out.data_ptr(), 1, 641, H, dh,
+                                      _stream()) != 0
+    assert lib.miclip_op_attention_q0(code, qkv.data_ptr(), out.data_ptr(), 1, N, H, 96,
+                                      _stream()) != 0
+
+
 def test_attention_bad_head_dim(lib):
     x = torch.zeros(3 * 96, device="cuda", dtype=torch.float16)
     y = torch.zeros(96, device="cuda", dtype=torch.float16)

@@ -151,6 +151,23 @@ def test_batch_invariance_and_shards():
     assert torch.equal(full, again), "encode is not deterministic"
 
 
+@pytest.mark.parametrize("name,dtype,tol", [("ViT-B/16", "fp16", 2e-5), ("ViT-B/32", "bf16", 2e-4),
+                                            ("ViT-L/14", "fp16", 2e-5)])
+def test_cls_last_block_matches_full(monkeypatch, name, dtype, tol):
+    """The last vision block on the CLS rows only (default) against the whole
+    block (MICLIP_CLS_LAST=0): the same features up to the CLS attention's
+    summation order (VALU dot products vs MFMA tiles)."""
+    from miclip.weights import synthetic_images
+    m = _model(name, dtype)
+    imgs = torch.from_numpy(synthetic_images(6, 224, seed=5)).cuda()
+    fast = m.encode_image(imgs).float().cpu()
+    monkeypatch.setenv("MICLIP_CLS_LAST", "0")
+    full = m.encode_image(imgs).float().cpu()
+    d = 1 - torch.nn.functional.cosine_similarity(fast, full, dim=1)
+    print(f"{name} {dtype}: 1-cos max {d.max().item():.2e}")
+    assert d.max().item() <= tol
+
+
 def test_normalize_and_proj_flags(golden):
     g = golden("vitb32")
     from miclip.weights import synthetic_images
