@@ -37,7 +37,8 @@ def main():
     ap.add_argument("--n", type=int, default=257)
     ap.add_argument("--warm", type=int, default=5)
     args = ap.parse_args()
-    lib = ctypes.CDLL(os.path.join(ROOT, "build", "stamps", f"libstamp_{args.kernel}.so"))
+    lib = ctypes.CDLL(os.environ.get("STAMP_LIB") or
+                      os.path.join(ROOT, "build", "stamps", f"libstamp_{args.kernel}.so"))
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     g = torch.Generator(device="cuda").manual_seed(0)
     W = 1024
