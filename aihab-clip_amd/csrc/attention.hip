@@ -78,21 +78,27 @@ struct HeadGeom {
 // of this lane's query; attend_store writes the normalised rows.
 // kt0 / kt_end: key-tile range (kt_end < 0: all tiles the chunk attends to);
 // m: the running max (scaled log2 domain) that lsum and O^T are relative to.
+// first / last: a key range processed in several calls starts the online
+// softmax state in the first call and reduces lsum across the lane halves in
+// the last one (both true: one call over the range).
 template <typename T, bool CAUSAL, int DH, bool PIPE = true>
 MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
                              const i16x8 (&qf)[HeadGeom<DH>::NKS], int chunk, int N, int Npad,
                              float c2, int lane, f32x16 (&o)[HeadGeom<DH>::NDT], float& lsum,
-                             float& m, int kt0 = 0, int kt_end = -1, int prio = 0) {
+                             float& m, int kt0 = 0, int kt_end = -1, int prio = 0,
+                             bool first = true, bool last = true) {
   using G = HeadGeom<DH>;
   const int l32 = lane & 31, hh = lane >> 5;
   const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
   const int q = chunk * 32 + l32;
-  m = -1e30f;
-  lsum = 0.f;
+  if (first) {
+    m = -1e30f;
+    lsum = 0.f;
 #pragma unroll
-  for (int r = 0; r < 16; ++r)
+    for (int r = 0; r < 16; ++r)
 #pragma unroll
-    for (int dt = 0; dt < G::NDT; ++dt) o[dt][r] = 0.f;
+      for (int dt = 0; dt < G::NDT; ++dt) o[dt][r] = 0.f;
+  }
   const int nkt_all = Npad >> 5;
   const int nkt = kt_end >= 0 ? kt_end
                               : (CAUSAL ? (chunk + 1 < nkt_all ? chunk + 1 : nkt_all) : nkt_all);
@@ -219,7 +225,79 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
       softmax_pv(kt, sa);
     }
   }
-  lsum = xor32_sum(lsum);
+  if (last) lsum = xor32_sum(lsum);
+}
+
+// Keys [key0, key0 + nkeys) (at most a few: the keys past the last full 32-key
+// tile, e.g. key 256 of N = 257) for one wave's 32 queries on VALU instead of a
+// 31/32-masked MFMA tile, continuing attend_chunk's online-softmax state (call
+// it with last = false and reduce lsum after). Lane (l32, hh) holds dims 16s +
+// 8hh + j of query l32 in qf[s][j] and O^T dims 32dt + 8(r>>2) + 4hh + (r&3) in
+// o[dt][r]: the score is a half-dot per lane summed across the lane halves
+// (v_dot2c_f32: exact fp16 products, fp32 sums), p = exp2(score*c2 - m) with
+// the same lazy rescale rule, P rounded to the compute dtype as the MFMA path's
+// B operand, and lsum counts p once (lane half 0). DH = 64 images (x8 kernel).
+template <typename T>
+MICLIP_DEV float dot2acc(uint32_t a, uint32_t b, float c);
+template <>
+MICLIP_DEV float dot2acc<_Float16>(uint32_t a, uint32_t b, float c) {
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  return __builtin_amdgcn_fdot2(__builtin_bit_cast(h2, a), __builtin_bit_cast(h2, b), c, false);
+}
+template <>
+MICLIP_DEV float dot2acc<__bf16>(uint32_t a, uint32_t b, float c) {
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(b2, a), __builtin_bit_cast(b2, b), c,
+                                         false);
+}
+
+template <typename T>
+MICLIP_DEV void attend_extra_keys(const char* kimg, const char* vimg, const i16x8 (&qf)[4],
+                                  f32x16 (&o)[2], float& lsum, float& m, int key0, int nkeys,
+                                  float c2, int lane) {
+  const int hh = lane >> 5;
+  for (int k = key0; k < key0 + nkeys; ++k) {
+    const char* kr = kimg + k * 128;
+    float part = 0.f;
+    // (memory clobbers keep the LDS reads from being hoisted together: the
+    // x8 kernel runs at its 128-VGPR cap)
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const u32x4 kv = *(const u32x4*)(kr + (((2 * st + hh) ^ ((k >> 1) & 7)) << 4));
+      const u32x4 qv = __builtin_bit_cast(u32x4, qf[st]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) part = dot2acc<T>(qv[e], kv[e], part);
+      asm volatile("" ::: "memory");
+    }
+    const float score = xor32_sum(part);
+    const float sc = score * c2;
+    if (!__all(sc - m <= 8.0f)) {
+      const float mnew = fmaxf(m, sc);
+      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+      m = mnew;
+      lsum *= alpha;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        o[0][r] *= alpha;
+        o[1][r] *= alpha;
+      }
+    }
+    const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(score, c2, -m));
+    if (hh == 0) lsum += p;
+    const float p16 = to_f<T>(to_t<T>(p));
+    const char* vr = vimg + k * 128;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int rq = 0; rq < 4; ++rq) {
+        const int ch = 4 * dt + rq;   // 16-B chunk of dims 32dt + 8rq .. +7
+        const i16x4 v = *(const i16x4*)(vr + ((ch ^ ((k & 3) << 1)) << 4) + 8 * hh);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          o[dt][4 * rq + e] = __builtin_fmaf(p16, from_bits<T>(v[e]), o[dt][4 * rq + e]);
+        asm volatile("" ::: "memory");
+      }
+  }
 }
 
 template <typename T, int DH>
@@ -468,10 +546,12 @@ __global__ __launch_bounds__(SPLIT ? 512 : 640) void attention_pipe_kernel(
 // K/V (LDS-DMA) the other computes, and 4 waves per SIMD hide the softmax /
 // LDS latencies that 2-3 waves of one workgroup leave exposed (the register
 // budget is 128 VGPRs: __launch_bounds__(512, 4)). Wave w owns query chunk w
-// (8 x 32 queries) and, flash-decoding style, key tiles [w*T/8, (w+1)*T/8) of
-// the ragged last chunk (N - 256 queries: the 257th token); its partial
-// (m, l, o) per valid query goes to LDS and, after the head's closing
-// barrier, wave v merges queries v, v+8, ... in a fixed order.
+// (8 x 32 queries) over the 8 full key tiles plus the N - 256 keys past them
+// on VALU (attend_extra_keys: no 31/32-masked ninth tile) and, flash-decoding
+// style, key tile w of the ragged last chunk (N - 256 queries: the 257th
+// token; wave 7 also its extra keys); its partial (m, l, o) per valid query
+// goes to LDS and, after the head's closing barrier, wave v merges queries v,
+// v+8, ... in a fixed order.
 // ---------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restrict__ qkv,
@@ -486,7 +566,8 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ntiles = Npad >> 5;              // key tiles (= query chunks incl. the ragged one)
   const int nvalid = N - 256;                // queries of the ragged chunk 8 (0 = none)
-  const int xkt0 = wave * ntiles / 8, xkt1 = (wave + 1) * ntiles / 8;
+  const int nextra = N - 256;                // keys past the 8 full tiles (attend_extra_keys)
+  (void)ntiles;
   float* part = (float*)(smem + 2 * img_bytes);   // [8 waves][nvalid][66]
   const int D = H * 64, ld = 3 * D;
   const float c2 = qk_scale * kLog2e;
@@ -522,8 +603,10 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
     {
       f32x16 o[2];
       float lsum, m;
-      attend_chunk<T, false, 64, false>(kimg, vimg, qf, wave, N, Npad, c2, lane, o, lsum, m, 0,
-                                        -1, prio);
+      attend_chunk<T, false, 64, false>(kimg, vimg, qf, wave, N, Npad, c2, lane, o, lsum, m, 0, 8,
+                                        prio, true, false);
+      attend_extra_keys<T>(kimg, vimg, qf, o, lsum, m, 256, nextra, c2, lane);
+      lsum = xor32_sum(lsum);
       MICLIP_STAMP(1);   // the wave's full query chunk
       attend_store<T, 64>(o, lsum, wave, N, obase, D, lane);
       MICLIP_STAMP(2);   // its output stores
@@ -532,8 +615,9 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
       load_q<T, 64>(qf, base, ld, 8, N, lane);
       f32x16 o[2];
       float lsum, m;
-      attend_chunk<T, false, 64, false>(kimg, vimg, qf, 8, N, Npad, c2, lane, o, lsum, m, xkt0,
-                                        xkt1, prio);
+      // key tile `wave` of the 8 full ones (the keys past them: in the merge)
+      attend_chunk<T, false, 64, false>(kimg, vimg, qf, 8, N, Npad, c2, lane, o, lsum, m, wave,
+                                        wave + 1, prio);
       // lane (l32, hh) holds O^T rows d = (r&3) + 8*(r>>2) + 4*hh (+32 in o[1]) of query l32
       const int l32 = lane & 31, hh = lane >> 5;
       if (l32 < nvalid) {
@@ -554,13 +638,29 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     MICLIP_STAMP(4);     // closing barrier
-    // merge the ragged chunk: wave v takes queries v, v+8, ...; lane = output dim
+    // merge the ragged chunk: wave v takes queries v, v+8, ...; lane = output
+    // dim. The keys past the 8 full tiles join as a ninth partial computed here
+    // (lane = dim: the dot product by a wave sum; K / V rows still resident).
     for (int c = wave; c < nvalid; c += 8) {
       const float* pc = part + (size_t)c * 66;
-      float mx = -1e30f;
+      const float qd = to_f<T>(base[(size_t)(256 + c) * ld + lane]);
+      float me = -1e30f, le = 0.f, oe = 0.f;
+      for (int k = 256; k < N; ++k) {
+        const int ch = (lane >> 3);
+        const float kd = to_f<T>(*(const T*)(kimg + k * 128 + ((ch ^ ((k >> 1) & 7)) << 4) + (lane & 7) * 2));
+        const float sc = wave_sum(qd * kd) * c2;
+        const float mn = fmaxf(me, sc), al = __builtin_amdgcn_exp2f(me - mn);
+        const float p = __builtin_amdgcn_exp2f(sc - mn);
+        const float vd = to_f<T>(*(const T*)(vimg + k * 128 + ((ch ^ ((k & 3) << 1)) << 4) + (lane & 7) * 2));
+        le = le * al + p;
+        oe = oe * al + to_f<T>(to_t<T>(p)) * vd;
+        me = mn;
+      }
+      float mx = me;
 #pragma unroll
       for (int i = 0; i < 8; ++i) mx = fmaxf(mx, pc[(size_t)i * nvalid * 66 + 64]);
-      float l = 0.f, acc = 0.f;
+      const float we = __builtin_amdgcn_exp2f(me - mx);
+      float l = we * le, acc = we * oe;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float* pi = pc + (size_t)i * nvalid * 66;
@@ -589,20 +689,6 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
 // (whose B operand it is there), P.V accumulated in fp32 with lane = output
 // dim pair; out: compact [B, H*dh] (row b = image b's CLS row).
 // ---------------------------------------------------------------------------
-template <typename T>
-MICLIP_DEV float dot2acc(uint32_t a, uint32_t b, float c);
-template <>
-MICLIP_DEV float dot2acc<_Float16>(uint32_t a, uint32_t b, float c) {
-  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-  return __builtin_amdgcn_fdot2(__builtin_bit_cast(h2, a), __builtin_bit_cast(h2, b), c, false);
-}
-template <>
-MICLIP_DEV float dot2acc<__bf16>(uint32_t a, uint32_t b, float c) {
-  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
-  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(b2, a), __builtin_bit_cast(b2, b), c,
-                                         false);
-}
-
 constexpr int kQ0MaxN = 640;   // keys per head (10 per lane)
 
 template <typename T, int DH>
