@@ -594,11 +594,13 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
       glds16_hidden(base + (size_t)r * ld + (isv ? 2 * D : D) + lch * 8,
                     (isv ? vimg : kimg) + piece * 1024);
     }
+    MICLIP_STAMP(6);   // DMA issue
     i16x8 qf[4];
     load_q<T, 64>(qf, base, ld, wave, N, lane);
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
+    MICLIP_STAMP(7);   // Q loads + wait for everything
     __builtin_amdgcn_s_barrier();
-    MICLIP_STAMP(0);   // K/V DMA + Q loads, their wait, the barrier
+    MICLIP_STAMP(0);   // the barrier
     T* obase = out + (size_t)b * N * D + h * 64;
     {
       f32x16 o[2];

@@ -24,7 +24,8 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 SEGS = {
     "gemm": ["tile_top", "main_loop", "boundary", "epilogue", "row_tail"],
-    "attn": ["kv_load_wait", "chunk", "store", "ragged", "close_barrier", "merge"],
+    "attn": ["kv_load_wait", "chunk", "store", "ragged", "close_barrier", "merge", "dma_issue",
+             "q_load_and_wait"],
 }
 
 
