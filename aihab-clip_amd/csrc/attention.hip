@@ -683,15 +683,16 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
 // One query per (image, head): token row 0 (CLS) only. The vision tower's last
 // block feeds nothing but the CLS rows forward (VisionTransformer.forward,
 // clip/model.py:226-229: ln_post(x[:, 0, :])), so there the attention of the
-// other N-1 queries is dead work. One wave per (image, head), four per
-// workgroup, all on VALU (1 x N x dh MACs per head; the K / V rows stream from
-// the QKV buffer). Lane l scores keys l, l+64, ... with v_dot2c_f32_{f16,bf16}
-// (fp32 sums of the exact fp16 products), exponentials in base 2 relative to
-// the row max, P rounded to the compute dtype for P.V as in the MFMA kernels
-// (whose B operand it is there), P.V accumulated in fp32 with lane = output
-// dim pair; out: compact [B, H*dh] (row b = image b's CLS row).
+// other N-1 queries is dead work. One workgroup (4 waves) per (image, head),
+// on VALU (1 x N x dh MACs per head; K / V rows stream from the QKV buffer):
+// thread t scores keys t, t+256, .. with v_dot2c_f32_{f16,bf16} (fp32 sums of
+// the exact fp16 products), exponentials in base 2 relative to the row max,
+// P rounded to the compute dtype for P.V as in the MFMA kernels (whose B
+// operand it is there); P.V by (key group, output dim pair) threads in fp32,
+// the key groups summed in a fixed order. out: compact [B, H*dh] (row b =
+// image b's CLS row).
 // ---------------------------------------------------------------------------
-constexpr int kQ0MaxN = 640;   // keys per head (10 per lane)
+constexpr int kQ0MaxN = 768;   // keys per head (3 per thread)
 
 template <typename T, int DH>
 __global__ __launch_bounds__(256) void attention_q0_kernel(const T* __restrict__ qkv,
@@ -699,12 +700,12 @@ __global__ __launch_bounds__(256) void attention_q0_kernel(const T* __restrict__
                                                            int H, float c2) {
   constexpr int NV = DH / 8;          // 16-B vectors per row
   constexpr int NP = DH / 2;          // output dim pairs
-  constexpr int KPI = 64 / NP;        // keys per P.V step (2 for dh 64, 1 for dh 80)
-  constexpr int NJ = kQ0MaxN / 64;    // key passes
-  const int lane = threadIdx.x & 63;
-  const int bh = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (bh >= B * H) return;            // whole wave
-  const int b = bh / H, h = bh - b * H;
+  constexpr int KG = 256 / NP;        // key groups of the P.V step (8 for dh 64, 6 for 80)
+  constexpr int NJ = kQ0MaxN / 256;   // key passes
+  __shared__ float sp[kQ0MaxN];       // p per key
+  __shared__ float red[KG][DH];       // per key group partial P.V; [0][0..7]: reductions
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
   const int D = H * DH, ld = 3 * D;
   const T* base = qkv + (size_t)b * N * ld + h * DH;
   u32x4 qv[NV];
@@ -714,9 +715,9 @@ __global__ __launch_bounds__(256) void attention_q0_kernel(const T* __restrict__
   float mx = -INFINITY;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int k = lane + 64 * j;
+    const int k = t + 256 * j;
     float a = -INFINITY;
-    if (64 * j < N) {                 // wave-uniform pass guard
+    if (256 * j < N) {                // block-uniform pass guard
       const T* kr = base + (size_t)(k < N ? k : N - 1) * ld + D;
       u32x4 kv[NV];
 #pragma unroll
@@ -731,46 +732,46 @@ __global__ __launch_bounds__(256) void attention_q0_kernel(const T* __restrict__
     sc[j] = a;
     mx = fmaxf(mx, a);
   }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-  float lsum = 0.f;
+  float* rw = &red[0][0];
+  mx = wave_max(mx);
+  if (lane == 0) rw[wave] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(rw[0], rw[1]), fmaxf(rw[2], rw[3]));
+  float ls = 0.f;
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const float pj = __builtin_amdgcn_exp2f(sc[j] - mx);   // exp2(-inf) = 0 past N
-    sc[j] = pj;
-    lsum += pj;
+    ls += pj;
+    if (t + 256 * j < kQ0MaxN) sp[t + 256 * j] = pj;
   }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) lsum += __shfl_xor(lsum, o);
-  // P.V: lane (sub, dp) = key parity sub, output dims 2dp, 2dp+1
-  const int sub = lane / NP, dp = lane - sub * NP;
-  const bool act = sub < KPI;
+  ls = wave_sum(ls);
+  __syncthreads();                    // everyone read rw[0..3] (max) before reuse
+  if (lane == 0) rw[4 + wave] = ls;
+  // P.V: thread (g, dp), g < KG: keys k = g, g + KG, ..; output dims 2dp, 2dp+1
+  const int g = t / NP, dp = t - g * NP;
   float a0 = 0.f, a1 = 0.f;
-  const T* vb = base + 2 * D + 2 * dp;
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    if (64 * j >= N) break;           // wave-uniform
-    for (int kk = 0; kk < 64; kk += KPI) {
-      const int src = kk + (act ? sub : 0);
-      const float pk = __shfl(sc[j], src);
-      const int k = 64 * j + src;
-      if (act && k < N) {
-        const uint32_t v = *(const uint32_t*)(vb + (size_t)k * ld);
-        const float p16 = to_f<T>(to_t<T>(pk));
-        a0 = __builtin_fmaf(p16, from_bits<T>((short)(v & 0xffff)), a0);
-        a1 = __builtin_fmaf(p16, from_bits<T>((short)(v >> 16)), a1);
-      }
+  if (g < KG) {
+    const T* vb = base + 2 * D + 2 * dp;
+    for (int k = g; k < N; k += KG) {
+      const uint32_t v = *(const uint32_t*)(vb + (size_t)k * ld);
+      const float p16 = to_f<T>(to_t<T>(sp[k]));
+      a0 = __builtin_fmaf(p16, from_bits<T>((short)(v & 0xffff)), a0);
+      a1 = __builtin_fmaf(p16, from_bits<T>((short)(v >> 16)), a1);
     }
   }
-  if constexpr (KPI == 2) {           // the two key parities' partial sums
-    a0 += __shfl_xor(a0, 32);
-    a1 += __shfl_xor(a1, 32);
+  __syncthreads();                    // rw[4..7] visible; sp reads done
+  const float lsum = (rw[4] + rw[5]) + (rw[6] + rw[7]);
+  __syncthreads();                    // before red[] is overwritten below
+  if (g < KG) {
+    red[g][2 * dp] = a0;
+    red[g][2 * dp + 1] = a1;
   }
-  if (lane < NP) {
-    const float inv = 1.0f / lsum;
-    const uint32_t w = (uint32_t)(uint16_t)to_bits<T>(a0 * inv) |
-                       ((uint32_t)(uint16_t)to_bits<T>(a1 * inv) << 16);
-    *(uint32_t*)(out + (size_t)b * D + h * DH + 2 * dp) = w;
+  __syncthreads();
+  if (t < DH) {
+    float o = 0.f;
+#pragma unroll
+    for (int q = 0; q < KG; ++q) o += red[q][t];
+    out[(size_t)b * D + h * DH + t] = to_t<T>(o / lsum);
   }
 }
 
@@ -921,7 +922,7 @@ hipError_t attention_q0(int dtype, const void* qkv, void* out, int B, int N, int
   if (B < 1 || N < 1 || H < 1 || N > kQ0MaxN) return hipErrorInvalidValue;
   if (head_dim == 0) head_dim = 64;
   if (head_dim != 64 && head_dim != 80) return hipErrorInvalidValue;
-  const int grid = (B * H + 3) / 4;
+  const int grid = B * H;
   const float c2 = kLog2e / sqrtf((float)head_dim);
   if (dtype == kF16) {
     if (head_dim == 64)

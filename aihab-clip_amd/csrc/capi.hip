@@ -515,7 +515,7 @@ int encode_image_part(miclip_model* m, Workspace w, const float* images, int B, 
   }
   // the last block on the CLS rows only (run_block); MX-fp8 models and (never
   // for CLIP's towers) N beyond attention_q0's range run it whole
-  const bool cls_last = cls_last_block() && !m->mx && N <= 640;
+  const bool cls_last = cls_last_block() && !m->mx && N <= 768;
   for (int l = 0; l < c.vision_layers; ++l)
     if ((rc = run_block(m, m->vblocks[l], w, B, N, W, H, dh, 0, s,
                         cls_last && l == c.vision_layers - 1)))

@@ -88,7 +88,7 @@ hipError_t attention(int dtype, const void* qkv, void* out, int B, int N, int H,
                      hipStream_t s, int variant = 0, int head_dim = 64);
 
 // Attention of token row 0 (CLS) of every image only: out [B, H*dh] compact
-// (row b = image b's CLS row), same qkv layout; N <= 640, dh 64 or 80 (0 = 64).
+// (row b = image b's CLS row), same qkv layout; N <= 768, dh 64 or 80 (0 = 64).
 hipError_t attention_q0(int dtype, const void* qkv, void* out, int B, int N, int H,
                         hipStream_t s, int head_dim = 64);
 

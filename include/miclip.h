@@ -268,7 +268,7 @@ int miclip_op_attention(int32_t dtype, const void* qkv, void* out, int32_t B, in
 /* Attention of the first query (token row 0, CLS) of every image only, same qkv
  * layout as miclip_op_attention; out [B, H*dh] compact (row b = image b's CLS
  * row). The vision tower's last block (only its CLS rows reach ln_post,
- * clip/model.py:226-229). N <= 640, dh 64 or 80 (0 = 64), non-causal. */
+ * clip/model.py:226-229). N <= 768, dh 64 or 80 (0 = 64), non-causal. */
 int miclip_op_attention_q0(int32_t dtype, const void* qkv, void* out, int32_t B, int32_t N,
                            int32_t H, int32_t head_dim, void* stream);
 

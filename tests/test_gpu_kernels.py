@@ -282,7 +282,7 @@ def test_attention_dh80(lib, dt, B, N, H, causal):
 
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
 @pytest.mark.parametrize("B,N,H,dh", [(3, 257, 16, 64), (2, 577, 16, 64), (5, 50, 12, 64),
-                                      (2, 257, 16, 80), (1, 1, 1, 64), (2, 640, 2, 64),
+                                      (2, 257, 16, 80), (1, 1, 1, 64), (2, 640, 2, 64), (1, 768, 2, 80),
                                       (7, 197, 3, 64), (1, 65, 5, 80)])
 def test_attention_q0(lib, dt, B, N, H, dh):
     """CLS-query attention (the vision tower's last block): row 0 of each image
@@ -299,7 +299,7 @@ def test_attention_q0(lib, dt, B, N, H, dh):
     assert err < (4e-2 if dt == "bf16" else 6e-3), err
     assert bool((out[B] == 7.0).all())
     # out of range: N beyond the kernel's key capacity, head dims other than 64 / 80
-    assert lib.miclip_op_attention_q0(code, qkv.data_ptr(), out.data_ptr(), 1, 641, H, dh,
+    assert lib.miclip_op_attention_q0(code, qkv.data_ptr(), out.data_ptr(), 1, 769, H, dh,
                                       _stream()) != 0
     assert lib.miclip_op_attention_q0(code, qkv.data_ptr(), out.data_ptr(), 1, N, H, 96,
                                       _stream()) != 0
