@@ -136,6 +136,20 @@ MICLIP_DEV void glds16(const void* g, void* lds) {
 // hipcc then never waits vmcnt(0) for it before an unrelated ds_read or load
 // (it cannot prove the LDS ranges disjoint). The caller retires it with its
 // own `s_waitcnt vmcnt` + barrier. `lds` must be wave-uniform.
+// 4-B form (each lane one dword, 256 B per wave): per-lane clamped sources at
+// row granularity (the persistent GEMM's row statistics).
+MICLIP_DEV void glds4_hidden(const void* g, const void* lds) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane(
+      (unsigned)(size_t)(const LDS_AS void*)lds);
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g), "s"(dst)
+      : "memory");
+}
+
 MICLIP_DEV void glds16_hidden(const void* g, const void* lds) {
   const unsigned dst = __builtin_amdgcn_readfirstlane(
       (unsigned)(size_t)(const LDS_AS void*)lds);

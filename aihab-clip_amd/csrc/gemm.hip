@@ -922,6 +922,35 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (TR) {
+      // This tile's epilogue operands (bias, and for the folded LN the column
+      // sums and the 256 row statistics) go to LDS by DMA now, one 1-KiB piece
+      // per wave 0-3, ahead of the K-tile stages: the main loop's first counted
+      // wait (wr = 0 waves, K-tile 1) retires them and its barriers publish
+      // them, so the tile boundary waits on no load. (Their last readers, the
+      // previous tile's epilogue, are past its closing barrier.) The 512
+      // statistics words go one per lane over the 8 waves, each row clamped to
+      // M - 1 (rows past M are never stored). The lane offset is made opaque
+      // so hipcc builds each 64-bit source address at its DMA instead of
+      // hoisting (and spilling) it.
+      int lo = lane;
+      asm volatile("" : "+v"(lo));
+      if (wave == 0) {
+        if (epi.bias) {
+          glds16_hidden(epi.bias + n0 + lo * 4, tbias);
+        } else {
+          float z;   // materialised here (a hoisted zero vector got spilled)
+          asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+          tbias[lane] = make_float4(z, z, z, z);
+        }
+      }
+      if constexpr (IsLN<Epi>::value) {
+        if (wave == 1) glds16_hidden(epi.colsum + n0 + lo * 4, tcs);
+        const int d = wave * 64 + lo, r = m0 + (d >> 1);
+        glds4_hidden((const float*)(epi.stats + (r < M ? r : M - 1)) + (d & 1),
+                     (const char*)tst + wave * 256);
+      }
+    }
     if (prev_stores < 0) {
       stage(0, 0);
       stage(3, 0);
@@ -974,31 +1003,6 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
     }
     if (wr == 0) lds_barrier();   // balance the stagger barrier
     MICLIP_STAMP(1);              // main loop
-    if constexpr (TR) {
-      // the tile's epilogue operands, parked in LDS before the barrier below
-      // publishes them (their last readers, the previous tile's epilogue, are
-      // many barriers back); loaded and retired here, before anything else is
-      // in flight (a load left pending makes hipcc drain the prefetch later)
-      if (tid < 64) {
-        const float4 b = epi.bias4nb(n0 + tid * 4);
-        asm volatile("" ::"v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w));
-        tbias[tid] = b;
-      }
-      if constexpr (IsLN<Epi>::value) {
-        if (tid < 64) {
-          const float4 c = epi.colsum4nb(n0 + tid * 4);
-          asm volatile("" ::"v"(c.x), "v"(c.y), "v"(c.z), "v"(c.w));
-          tcs[tid] = c;
-        }
-        if (tid < 256) {
-          const int sr = m0 + tid;
-          const float2 st = epi.stats[sr < M ? sr : M - 1];
-          asm volatile("" ::"v"(st.x), "v"(st.y));
-          tst[tid] = st;
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
 
     // ---- tile boundary: prefetch the next tile's K-tile 0 into buffer 0 ----
     lds_barrier();                 // every wave is done with both buffers
