@@ -1073,7 +1073,9 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
             }
           }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        MICLIP_STAMP(5);              // epilogue math + staging writes
         lds_barrier();
+        MICLIP_STAMP(6);              // staging barrier
         // readback: wave w stores image rows 16w .. 16w+15 in pairs (R, R+1). Lane
         // (h, li) reads the 8 bytes at image half h of both rows (columns 8li + 4h
         // .. +3); one v_permlane32_swap per dword then leaves lanes 0-31 with row R
@@ -1102,6 +1104,7 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
             if (full || row < M) *(u32x4*)(cb + (size_t)row * epi.ldc) = w;
           }
         }
+        MICLIP_STAMP(7);              // readback + store issue
       }
     } else {
     // ---- epilogue: 4 passes of 64 rows staged at STG ----

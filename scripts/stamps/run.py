@@ -23,7 +23,8 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 SEGS = {
-    "gemm": ["tile_top", "main_loop", "boundary", "epilogue", "row_tail"],
+    "gemm": ["tile_top", "main_loop", "boundary", "epilogue", "row_tail", "epi_math_stage",
+             "epi_barrier", "epi_readback_store"],
     "attn": ["kv_load_wait", "chunk", "store", "ragged", "close_barrier", "merge", "dma_issue",
              "q_load_and_wait"],
 }
@@ -37,6 +38,7 @@ def main():
     ap.add_argument("--b", type=int, default=128)
     ap.add_argument("--n", type=int, default=257)
     ap.add_argument("--warm", type=int, default=5)
+    ap.add_argument("--null", action="store_true", help="gemm: the no-output epilogue (epi 3)")
     args = ap.parse_args()
     lib = ctypes.CDLL(os.environ.get("STAMP_LIB") or
                       os.path.join(ROOT, "build", "stamps", f"libstamp_{args.kernel}.so"))
@@ -54,7 +56,12 @@ def main():
                           torch.rand(M, device="cuda", generator=g) + 0.5], 1).contiguous()
         C = torch.empty(M, N, device="cuda", dtype=torch.float16)
         flops = 2.0 * M * N * K
-        if args.shape in ("qkv", "fc"):
+        if args.null:
+            Cf = torch.empty(M, N, device="cuda", dtype=torch.float32)
+            fn = lambda: lib.miclip_op_gemm(0, ctypes.c_void_p(A.data_ptr()), ctypes.c_void_p(Wt.data_ptr()),
+                                            ctypes.c_void_p(bias.data_ptr()), ctypes.c_void_p(Cf.data_ptr()),
+                                            M, N, K, 3, 0, 0, s)
+        elif args.shape in ("qkv", "fc"):
             act = int(args.shape == "fc")
             fn = lambda: lib.miclip_op_gemm_ln(0, ctypes.c_void_p(A.data_ptr()), ctypes.c_void_p(Wt.data_ptr()),
                                                ctypes.c_void_p(bias.data_ptr()), ctypes.c_void_p(colsum.data_ptr()),
