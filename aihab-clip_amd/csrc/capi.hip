@@ -381,6 +381,15 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
     MICLIP_HIP(attention_q0(dt, w.qkv, w.o, items, N, H, s, dh));
     MICLIP_HIP(gather_rows(w.x, w.xc, items, N, W, r16 ? 2 : 4, s));
     MICLIP_HIP(gemm_residual(dt, w.o, b.w_out, b.b_out, w.xc, items, W, W, s, 0, r16));
+    if (mx) {   // MX-fp8 MLP on the CLS rows (their scale blocks are row-local)
+      MICLIP_HIP(layernorm(dt, w.xc, nullptr, 1, b.ln2_g, b.ln2_b, nullptr, nullptr, items, W, 0,
+                           s, r16, w.hq, w.hs));
+      MICLIP_HIP(gemm_mx(w.hq, w.hs, b.w_fc, b.s_fc, b.b_fc, w.fq, w.fs, items, 4 * W, W, 5,
+                         m->cfg.act, s));
+      MICLIP_HIP(gemm_mx(w.fq, w.fs, b.w_proj, b.s_proj, b.b_proj, w.xc, nullptr, items, W, 4 * W,
+                         1, ACT_NONE, s));
+      return 0;
+    }
     if (fold) {
       MICLIP_HIP(ln_stats(w.xc, w.stats, items, W, s, b.fs_fc));
       MICLIP_HIP(gemm_store_ln(dt, w.xc, b.wf_fc, b.c_fc, b.cs_fc, w.stats, w.f, items, 4 * W, W,
@@ -513,9 +522,9 @@ int encode_image_part(miclip_model* m, Workspace w, const float* images, int B, 
                          m->resid16 ? nullptr : (float*)w.x, m->resid16 ? w.x : nullptr, M, W,
                          0, s, m->resid16));
   }
-  // the last block on the CLS rows only (run_block); MX-fp8 models and (never
-  // for CLIP's towers) N beyond attention_q0's range run it whole
-  const bool cls_last = cls_last_block() && !m->mx && N <= 768;
+  // the last block on the CLS rows only (run_block); N beyond attention_q0's
+  // range (never for CLIP's towers) runs it whole
+  const bool cls_last = cls_last_block() && N <= 768;
   for (int l = 0; l < c.vision_layers; ++l)
     if ((rc = run_block(m, m->vblocks[l], w, B, N, W, H, dh, 0, s,
                         cls_last && l == c.vision_layers - 1)))

@@ -152,7 +152,7 @@ def test_batch_invariance_and_shards():
 
 
 @pytest.mark.parametrize("name,dtype,tol", [("ViT-B/16", "fp16", 2e-5), ("ViT-B/32", "bf16", 2e-4),
-                                            ("ViT-L/14", "fp16", 2e-5)])
+                                            ("ViT-L/14", "fp16", 2e-5), ("ViT-H-14", "mxfp8", 1e-3)])
 def test_cls_last_block_matches_full(monkeypatch, name, dtype, tol):
     """The last vision block on the CLS rows only (default) against the whole
     block (MICLIP_CLS_LAST=0): the same features up to the CLS attention's
