@@ -573,7 +573,9 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
   const float c2 = qk_scale * kLog2e;
   const int bh0 = blockIdx.x * hpw;
   const int nh = (B * H - bh0) < hpw ? (B * H - bh0) : hpw;
-  const int pieces = Npad / 8;
+  // 1-KiB pieces (8 key rows) per image: only rows < N are ever read (the full
+  // tiles cover 0..255, keys past them go through attend_extra_keys / the merge)
+  const int pieces = (N + 7) / 8;
   const int prow = lane >> 3, pch = lane & 7;
   auto head_base = [&](int bh) {
     const int b = bh / H, h = bh - b * H;
