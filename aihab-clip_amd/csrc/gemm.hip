@@ -499,7 +499,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
 
   const int nk = K / 64;
   i16x8 af[2][4], bf[2][2];
-  auto quadrant = [&](const char* sa, const char* sb, int qi, int qj, bool load_a) {
+  auto quadrant = [&](const char* sa, const char* sb, int qi, int qj, bool load_a,
+                      bool load_b = true) {
     if (load_a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -507,10 +508,12 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
         af[1][i] = *(const i16x8*)(sa + i * 2048 + sw1);
       }
     }
+    if (load_b) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      bf[0][j] = *(const i16x8*)(sb + j * 2048 + sw0);
-      bf[1][j] = *(const i16x8*)(sb + j * 2048 + sw1);
+      for (int j = 0; j < 2; ++j) {
+        bf[0][j] = *(const i16x8*)(sb + j * 2048 + sw0);
+        bf[1][j] = *(const i16x8*)(sb + j * 2048 + sw1);
+      }
     }
   };
   auto mfma_q = [&](int qi, int qj) {
@@ -571,7 +574,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
         }
         const int qi = (p >= 2) ? 1 : 0;
         const int qj = (p == 1 || p == 2) ? 1 : 0;
-        quadrant(qi ? sA1 : sA0, qj ? sB1 : sB0, qi, qj, p == 0 || p == 2);
+        quadrant(qi ? sA1 : sA0, qj ? sB1 : sB0, qi, qj, p == 0 || p == 2, p != 2);
         if (p == 0 && t + 1 < nk) stage(1, t + 1);
         if (p == 1 && t + 1 < nk) stage(2, t + 1);
         if (p == 2 && t + 2 < nk) stage(0, t + 2);
@@ -879,7 +882,9 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
 
   f32x4 acc[2][2][4][2];
   i16x8 af[2][4], bf[2][2];
-  auto quadrant = [&](const char* sa, const char* sb, bool load_a) {
+  // phase 2 = (A1, B1) finds B1 still in bf from phase 1 (same K-tile buffer):
+  // load_b = false there, 28 fragment reads per K-tile instead of 32
+  auto quadrant = [&](const char* sa, const char* sb, bool load_a, bool load_b) {
     if (load_a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -887,10 +892,12 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
         af[1][i] = *(const i16x8*)(sa + i * 2048 + sw1);
       }
     }
+    if (load_b) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      bf[0][j] = *(const i16x8*)(sb + j * 2048 + sw0);
-      bf[1][j] = *(const i16x8*)(sb + j * 2048 + sw1);
+      for (int j = 0; j < 2; ++j) {
+        bf[0][j] = *(const i16x8*)(sb + j * 2048 + sw0);
+        bf[1][j] = *(const i16x8*)(sb + j * 2048 + sw1);
+      }
     }
   };
   auto mfma_q = [&](int qi, int qj) {
@@ -990,7 +997,7 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
         }
         const int qi = (p >= 2) ? 1 : 0;
         const int qj = (p == 1 || p == 2) ? 1 : 0;
-        quadrant(qi ? sA1 : sA0, qj ? sB1 : sB0, p == 0 || p == 2);
+        quadrant(qi ? sA1 : sA0, qj ? sB1 : sB0, p == 0 || p == 2, p != 2);
         if (p == 0 && t + 1 < nk) stage(1, t + 1);
         if (p == 1 && t + 1 < nk) stage(2, t + 1);
         if (p == 2 && t + 2 < nk) stage(0, t + 2);
@@ -1327,7 +1334,9 @@ __global__ __launch_bounds__(512) void gemm256p_kernel(const T* __restrict__ A,
   float4 bv[2][2];
   load_bias_regs(epi, cn0, wc, lane, bv);
   i16x8 af[2][4], bf[2][2];
-  auto quadrant = [&](const char* sa, const char* sb, bool load_a) {
+  // phase 2 = (A1, B1) finds B1 still in bf from phase 1 (same K-tile buffer):
+  // load_b = false there, 28 fragment reads per K-tile instead of 32
+  auto quadrant = [&](const char* sa, const char* sb, bool load_a, bool load_b) {
     if (load_a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -1335,10 +1344,12 @@ __global__ __launch_bounds__(512) void gemm256p_kernel(const T* __restrict__ A,
         af[1][i] = *(const i16x8*)(sa + i * 2048 + sw1);
       }
     }
+    if (load_b) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      bf[0][j] = *(const i16x8*)(sb + j * 2048 + sw0);
-      bf[1][j] = *(const i16x8*)(sb + j * 2048 + sw1);
+      for (int j = 0; j < 2; ++j) {
+        bf[0][j] = *(const i16x8*)(sb + j * 2048 + sw0);
+        bf[1][j] = *(const i16x8*)(sb + j * 2048 + sw1);
+      }
     }
   };
   auto mfma_q = [&](int qi, int qj) {
@@ -1393,7 +1404,7 @@ __global__ __launch_bounds__(512) void gemm256p_kernel(const T* __restrict__ A,
       }
       const int qi = (p >= 2) ? 1 : 0;
       const int qj = (p == 1 || p == 2) ? 1 : 0;
-      quadrant(qi ? sA1 : sA0, qj ? sB1 : sB0, p == 0 || p == 2);
+      quadrant(qi ? sA1 : sA0, qj ? sB1 : sB0, p == 0 || p == 2, p != 2);
       if (p == 0 && g + 1 < total) stage(1, g + 1);
       if (p == 1 && g + 1 < total) stage(2, g + 1);
       if (p == 2 && g + 2 < total) stage(0, g + 2);

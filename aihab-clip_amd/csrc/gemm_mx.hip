@@ -171,13 +171,16 @@ __global__ __launch_bounds__(512) void gemm256_mx_kernel(const uint8_t* __restri
     const i32x4 lo = *(const i32x4*)p0, hi = *(const i32x4*)p1;
     return (v8i)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   };
-  auto quadrant = [&](const char* sa_, const char* sb_, bool load_a) {
+  // phase 2 = (A1, B1) finds B1 still in bf from phase 1: load_b = false there
+  auto quadrant = [&](const char* sa_, const char* sb_, bool load_a, bool load_b) {
     if (load_a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[i] = rd8(sa_ + i * 2048 + sw0, sa_ + i * 2048 + sw1);
     }
+    if (load_b) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) bf[j] = rd8(sb_ + j * 2048 + sw0, sb_ + j * 2048 + sw1);
+      for (int j = 0; j < 2; ++j) bf[j] = rd8(sb_ + j * 2048 + sw0, sb_ + j * 2048 + sw1);
+    }
   };
   auto mfma_q = [&](int qi, int qj) {
     // op_sel picks the scale byte: A slot qi*4 + i -> dword qi, byte i; W slot
@@ -247,7 +250,7 @@ __global__ __launch_bounds__(512) void gemm256_mx_kernel(const uint8_t* __restri
       }
       const int qi = (p >= 2) ? 1 : 0;
       const int qj = (p == 1 || p == 2) ? 1 : 0;
-      quadrant(qi ? sA1 : sA0, qj ? sB1 : sB0, p == 0 || p == 2);
+      quadrant(qi ? sA1 : sA0, qj ? sB1 : sB0, p == 0 || p == 2, p != 2);
       if (p == 0) {
         // this K-tile's scales (they arrived with A0(t)). Read from inline asm
         // that also retires them (lgkmcnt(0), which the phase waits for anyway):
