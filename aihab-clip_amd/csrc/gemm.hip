@@ -773,9 +773,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
 // tile; 0 for a partial tile, i.e. a full wait), never more than were issued.
 // The row tail runs at the end on the same workgroups (gemm_tail_wg tasks).
 // ---------------------------------------------------------------------------
-// global stores per lane of one tile's epilogue: 4 passes x 8 rows, or with
-// transposed accumulators 2 passes x 8 16-B stores
-template <class Epi, bool TR> struct EpiStores { static constexpr int n = TR ? 16 : 32; };
+// global stores per lane issued after the next-tile prefetch: the last 3 of the
+// 4 passes x 8 rows, or with transposed accumulators 2 passes x 8 16-B stores
+template <class Epi, bool TR> struct EpiStores { static constexpr int n = TR ? 16 : 24; };
 template <bool TR> struct EpiStores<EpiNull, TR> { static constexpr int n = 0; };
 
 // {mean, rstd} of rows r0, r0+8, ..., r0+56 (wave-uniform r0, all in bounds) by
@@ -810,6 +810,7 @@ MICLIP_DEV void wait_vmcnt_tile(int n) {
   switch (n) {
     case 36: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
     case 32: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+    case 28: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
     case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
@@ -1032,16 +1033,24 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
       if (tid < 64) lncs[tid] = sv;
     }
     const int nid = id + gridDim.x;
-    if (nid < ndp) {
-      sources(nid, m0, n0, asrc, bsrc);
+    auto prefetch_next = [&]() {
+      if (nid < ndp) {
+        sources(nid, m0, n0, asrc, bsrc);
 #pragma unroll
-      for (int kind = 0; kind < 4; ++kind) {
-        const T* const* src = kind < 2 ? asrc[kind] : bsrc[kind - 2];
-        char* dst = smem + kind * HALF + wave * 2048;
-        glds16_hidden(src[0], dst);
-        glds16_hidden(src[1], dst + 1024);
+        for (int kind = 0; kind < 4; ++kind) {
+          const T* const* src = kind < 2 ? asrc[kind] : bsrc[kind - 2];
+          char* dst = smem + kind * HALF + wave * 2048;
+          glds16_hidden(src[0], dst);
+          glds16_hidden(src[1], dst + 1024);
+        }
       }
-    }
+    };
+    // Issued inside the epilogue (TR: after the first pass's staging writes;
+    // otherwise after the first pass's stores), not here: hipcc puts a vmcnt(0)
+    // in front of the epilogue's first LDS read (it still counts the main
+    // loop's compiler-visible LDS-DMA as in flight), and issued here that wait
+    // also drained this prefetch -- every tile's epilogue started one DMA round
+    // trip late.
     const bool full = cm0 + 256 <= M;
     MICLIP_STAMP(2);              // tile boundary: epilogue operands, prefetch issue
     if constexpr (TR) {
@@ -1055,17 +1064,36 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
       // them as 512-B row segments. fp16 staging: half the LDS bytes of the
       // fp32 row staging, and no wave idles while another half stages.
       char* img = smem + STG;
+      // The epilogue operands are read from LDS up front -- the lane's 4 column
+      // quads of bias / column sums once per tile, its 4 row statistics once per
+      // pass -- before the pass's first staging write: a read placed after a
+      // ds_write to the same array waits for that write (hipcc cannot tell them
+      // apart), which serialised every 4-element group behind one LDS round trip
+      // and kept the exp -> rcp chains of different groups from interleaving.
+      float4 tb[2][2], tc[2][2];
+#pragma unroll
+      for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int c4 = wc * 16 + qj * 8 + j * 4 + fk;     // this lane's column quad
+          tb[qj][j] = tbias[c4];
+          tc[qj][j] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if constexpr (IsLN<Epi>::value) tc[qj][j] = tcs[c4];
+        }
 #pragma unroll
       for (int qi = 0; qi < 2; ++qi) {
         if (qi > 0) lds_barrier();   // pass 0's readers are done with the image
+        float2 ts[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          ts[i] = make_float2(0.f, 0.f);
+          if constexpr (IsLN<Epi>::value) ts[i] = tst[wr * 128 + qi * 64 + i * 16 + fr];
+        }
 #pragma unroll
         for (int qj = 0; qj < 2; ++qj)
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             const int c4 = wc * 16 + qj * 8 + j * 4 + fk;   // this lane's column quad
-            const float4 b = tbias[c4];
-            float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
-            if constexpr (IsLN<Epi>::value) cs = tcs[c4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const int ir = wr * 64 + i * 16 + fr;         // image row
@@ -1073,12 +1101,13 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
               const float4 v = make_float4(a[0], a[1], a[2], a[3]);
               i16x4 o;
               if constexpr (IsLN<Epi>::value)
-                o = epi.val4ln(v, b, cs, tst[wr * 128 + qi * 64 + i * 16 + fr]);
+                o = epi.val4ln(v, tb[qj][j], tc[qj][j], ts[i]);
               else
-                o = epi.val4(v, b);
+                o = epi.val4(v, tb[qj][j]);
               *(i16x4*)(img + ir * TLD + (c4 & 1) * 256 + (c4 >> 1) * 8) = o;
             }
           }
+        if (qi == 0) prefetch_next();   // before this pass's stores (prev_stores = 16)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         MICLIP_STAMP(5);              // epilogue math + staging writes
         lds_barrier();
@@ -1224,6 +1253,10 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
 #pragma unroll
         for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(xf[k]));
       }
+      // after the first pass's stores: hipcc's counted waits for the residual
+      // loads assume no hidden operation younger than them, so a prefetch issued
+      // before them made the first pass wait for it too (prev_stores = 24)
+      if (p == 0) prefetch_next();
     }
     }
     lds_barrier();                 // staging (buffer-1 half) free for the next tile
