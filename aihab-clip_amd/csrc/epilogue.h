@@ -258,8 +258,15 @@ template <typename T, int ACT> struct TrAcc<EpiStore<T, ACT>> : std::true_type {
 
 // Residual stream X (R = float, or _Float16 as in the reference's fp16 GPU
 // model, clip/model.py:184-185 `x = x + ...` on half tensors) += acc + bias.
-// fp16: one rounding of x + (acc + bias) (the reference rounds acc + bias
-// first), pinned by fin so the tile and tail paths round alike.
+// fp16: the reference's two roundings -- the projection's output t = fp16(acc +
+// bias), then the half-tensor add x + t, an IEEE fp16 add (v_pk_add_f16; for two
+// fp16 operands fp16(float(x) + float(t)) is the same value). Every path (the
+// persistent kernel's transposed-accumulator readback, put4x, put1) does exactly
+// this, so the tile and tail paths agree bit for bit.
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+MICLIP_DEV unsigned add_f16x2(unsigned a, unsigned b) {
+  return __builtin_bit_cast(unsigned, __builtin_bit_cast(h16x2, a) + __builtin_bit_cast(h16x2, b));
+}
 template <typename R>
 struct EpiResidual {
   R* X;
@@ -297,20 +304,34 @@ struct EpiResidual {
     *(f32x4*)(X + (size_t)r * ldx + c) =
         f32x4{x[0] + (v.x + b.x), x[1] + (v.y + b.y), x[2] + (v.z + b.z), x[3] + (v.w + b.w)};
   }
-  template <bool ASM = false>
-  MICLIP_DEV void put4x(int r, int c, float4 v, float4 b, i16x4 x) const {
-    // packed: (acc + b) then x + that, two v_pk_add_f32 per pair -- the same
-    // two roundings as put1's scalar form
-    const f32x2 t0 = (f32x2){v.x, v.y} + (f32x2){b.x, b.y};
-    const f32x2 t1 = (f32x2){v.z, v.w} + (f32x2){b.z, b.w};
-    f32x2 y0 = (f32x2){from_bits<R>(x[0]), from_bits<R>(x[1])} + t0;
-    f32x2 y1 = (f32x2){from_bits<R>(x[2]), from_bits<R>(x[3])} + t1;
+  // fp16 stream: the projection's 4 output elements t = fp16(acc + b), packed
+  // adds (v_pk_add_f32) then the conversion -- the value the transposed-
+  // accumulator epilogue stages; the residual add follows at readback (add_x)
+  MICLIP_DEV i16x4 val4(float4 v, float4 b) const {
+    f32x2 y0 = (f32x2){v.x, v.y} + (f32x2){b.x, b.y};
+    f32x2 y1 = (f32x2){v.z, v.w} + (f32x2){b.z, b.w};
     asm("" : "+v"(y0), "+v"(y1));
     i16x4 o;
     o[0] = to_bits<R>(y0[0]);
     o[1] = to_bits<R>(y0[1]);
     o[2] = to_bits<R>(y1[0]);
     o[3] = to_bits<R>(y1[1]);
+    return o;
+  }
+  // x + t on n fp16 pairs (dwords)
+  template <int NW>
+  MICLIP_DEV static void add_x(unsigned (&t)[NW], const unsigned (&x)[NW]) {
+#pragma unroll
+    for (int i = 0; i < NW; ++i) t[i] = add_f16x2(x[i], t[i]);
+  }
+  template <bool ASM = false>
+  MICLIP_DEV void put4x(int r, int c, float4 v, float4 b, i16x4 x) const {
+    const u32x2 t2 = __builtin_bit_cast(u32x2, val4(v, b));
+    const u32x2 x2 = __builtin_bit_cast(u32x2, x);
+    unsigned t[2] = {t2[0], t2[1]};
+    const unsigned xx[2] = {x2[0], x2[1]};
+    add_x<2>(t, xx);
+    const i16x4 o = __builtin_bit_cast(i16x4, (u32x2){t[0], t[1]});
     i16x4* p = (i16x4*)(X + (size_t)r * ldx + c);
     if constexpr (ASM)
       st_b64_asm(p, o);
@@ -322,7 +343,7 @@ struct EpiResidual {
     if constexpr (std::is_same_v<R, float>)
       *p = *p + (v + b);
     else
-      *p = to_t<R>(fin((float)*p + (v + b)));
+      *p = to_t<R>(fin((float)*p + from_bits<R>(to_bits<R>(fin(v + b)))));
   }
 };
 
@@ -330,6 +351,9 @@ struct EpiResidual {
 // staged epilogues prefetch those reads (load4 / put4x).
 template <class Epi> struct PrefetchX : std::false_type {};
 template <> struct PrefetchX<EpiResidual<_Float16>> : std::true_type {};
+// the fp16 residual stream runs the transposed-accumulator epilogue too: t is
+// staged, and x + t is formed at readback on row-contiguous 16-B pieces
+template <> struct TrAcc<EpiResidual<_Float16>> : std::true_type {};
 // fp32 residual rows (16 B per lane) are prefetched by the persistent kernel only
 // (8 rows per pass; the one-tile kernel's 16 would cost 64 VGPRs)
 template <class Epi> struct PrefetchXF : std::false_type {};

@@ -776,6 +776,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const T* __restrict__ A,
 // global stores per lane issued after the next-tile prefetch: the last 3 of the
 // 4 passes x 8 rows, or with transposed accumulators 2 passes x 8 16-B stores
 template <class Epi, bool TR> struct EpiStores { static constexpr int n = TR ? 16 : 24; };
+// fp16 residual, transposed: after the prefetch come pass 0's 8 stores, pass 1's
+// 8 residual loads and its 8 stores
+template <> struct EpiStores<EpiResidual<_Float16>, true> { static constexpr int n = 24; };
+// output of the transposed-accumulator epilogue: C, or the residual stream X
+template <class Epi> MICLIP_DEV auto* tr_out(const Epi& e) {
+  if constexpr (PrefetchX<Epi>::value) return e.X; else return e.C;
+}
+template <class Epi> MICLIP_DEV int tr_ld(const Epi& e) {
+  if constexpr (PrefetchX<Epi>::value) return e.ldx; else return e.ldc;
+}
 template <bool TR> struct EpiStores<EpiNull, TR> { static constexpr int n = 0; };
 
 // {mean, rstd} of rows r0, r0+8, ..., r0+56 (wave-uniform r0, all in bounds) by
@@ -1089,6 +1099,21 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
           ts[i] = make_float2(0.f, 0.f);
           if constexpr (IsLN<Epi>::value) ts[i] = tst[wr * 128 + qi * 64 + i * 16 + fr];
         }
+        // fp16 residual stream: the 8 x pieces this lane adds at readback (row
+        // R + h of each pair, columns 8li .. 8li+7: 16 B, row-contiguous), loaded
+        // now so their latency hides under the staging math (after the LDS reads
+        // above: hipcc's vmcnt(0) in front of the epilogue's first LDS read would
+        // otherwise wait for them)
+        u32x4 xq[8];
+        if constexpr (PrefetchX<Epi>::value) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int ir = wave * 16 + 2 * k + (lane >> 5);
+            const int row = cm0 + (ir >> 6) * 128 + qi * 64 + (ir & 63);
+            xq[k] = *(const u32x4*)(epi.X + (size_t)(row < M ? row : M - 1) * epi.ldx + cn0 +
+                                    (lane & 31) * 8);
+          }
+        }
 #pragma unroll
         for (int qj = 0; qj < 2; ++qj)
 #pragma unroll
@@ -1107,7 +1132,16 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
               *(i16x4*)(img + ir * TLD + (c4 & 1) * 256 + (c4 >> 1) * 8) = o;
             }
           }
-        if (qi == 0) prefetch_next();   // before this pass's stores (prev_stores = 16)
+        if (qi == 0) {
+          // the residual pieces are waited for before the prefetch is issued:
+          // waiting for them behind it would wait for the prefetch too (vmcnt
+          // retires in issue order)
+          if constexpr (PrefetchX<Epi>::value) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(xq[k]));
+          }
+          prefetch_next();   // before this pass's stores (prev_stores: EpiStores)
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         MICLIP_STAMP(5);              // epilogue math + staging writes
         lds_barrier();
@@ -1118,7 +1152,7 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
         // columns 8li .. 8li+7 and lanes 32-63 with row R+1 (guide T21): 16-B
         // stores, each half-wave writing one whole 512-B row segment.
         const int h = lane >> 5, li = lane & 31;
-        T* cb = epi.C + cn0 + li * 8;
+        auto* cb = tr_out(epi) + cn0 + li * 8;
 #pragma unroll
         for (int p0 = 0; p0 < 8; p0 += 2) {
           i16x4 va[2], vb[2];
@@ -1134,10 +1168,16 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
             const u32x2 a = __builtin_bit_cast(u32x2, va[p]), b = __builtin_bit_cast(u32x2, vb[p]);
             const auto s0 = __builtin_amdgcn_permlane32_swap(a[0], b[0], false, false);
             const auto s1 = __builtin_amdgcn_permlane32_swap(a[1], b[1], false, false);
-            const u32x4 w = {s0[0], s1[0], s0[1], s1[1]};
+            u32x4 w = {s0[0], s1[0], s0[1], s1[1]};
+            if constexpr (PrefetchX<Epi>::value) {   // x + t, 8 fp16 pairs of adds
+              unsigned t[4] = {w[0], w[1], w[2], w[3]};
+              const unsigned x[4] = {xq[p0 + p][0], xq[p0 + p][1], xq[p0 + p][2], xq[p0 + p][3]};
+              Epi::template add_x<4>(t, x);
+              w = (u32x4){t[0], t[1], t[2], t[3]};
+            }
             const int ir = wave * 16 + 2 * (p0 + p) + h;
             const int row = cm0 + (ir >> 6) * 128 + qi * 64 + (ir & 63);
-            if (full || row < M) *(u32x4*)(cb + (size_t)row * epi.ldc) = w;
+            if (full || row < M) *(u32x4*)(cb + (size_t)row * tr_ld(epi)) = w;
           }
         }
         MICLIP_STAMP(7);              // readback + store issue
