@@ -227,9 +227,11 @@ def test_zero_shot_head_vs_torch(B, C, k):
 
 
 # MICLIP_MXFP8: parity unpinned with respect to the
-# reference (no fp8 path there); bounded against the fp32 goldens with an fp8
-# tolerance instead of COS_TOL.
-MX_COS_TOL = 2e-2
+# reference (no fp8 path there); bounded against the fp32 goldens with fp8
+# tolerances instead of COS_TOL, set a few times above what the block-scaled
+# e4m3 path measures (image 1-cos <= 5.5e-4, text <= 4.9e-3).
+MX_COS_TOL_IMAGE = 2e-3
+MX_COS_TOL_TEXT = 1e-2
 
 
 @pytest.mark.parametrize("tag,name", [("vitb32", "ViT-B/32"), ("vith14", "ViT-H-14")])
@@ -244,4 +246,4 @@ def test_mxfp8_encode_within_fp8_tolerance(golden, tag, name):
     xb, xp = m.encode_text(torch.from_numpy(g["tokens"]).long().cuda())
     dt = _one_minus_cos(xp.cpu(), g["text_proj"])
     print(f"{tag}/mxfp8: image 1-cos max {d.max():.2e}, text 1-cos max {dt.max():.2e}")
-    assert d.max() <= MX_COS_TOL and dt.max() <= MX_COS_TOL
+    assert d.max() <= MX_COS_TOL_IMAGE and dt.max() <= MX_COS_TOL_TEXT
