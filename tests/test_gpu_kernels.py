@@ -309,3 +309,27 @@ def test_attention_bad_head_dim(lib):
     x = torch.zeros(3 * 96, device="cuda", dtype=torch.float16)
     y = torch.zeros(96, device="cuda", dtype=torch.float16)
     assert lib.miclip_op_attention(0, x.data_ptr(), y.data_ptr(), 1, 1, 1, 96, 0, 0, _stream()) != 0
+
+
+# The fp16 residual stream's rounding (clip/model.py:184-185 on half tensors):
+# t = fp16(A.W^T + b), then the half add x + t. Integer-valued operands make the
+# fp32 accumulation exact in any order, so every GEMM path -- the persistent
+# kernel's transposed-accumulator epilogue (tile rows), its row tail, the other
+# 256x256 schedules and the 128x128 kernel -- must match torch's own half-tensor
+# arithmetic bit for bit (|A.W^T + b| reaches ~10^4, so fp16(.) really rounds).
+@pytest.mark.parametrize("M,N,K,variant", [(16421, 1024, 1024, 0), (32896, 1024, 4096, 0),
+                                           (16448, 1024, 1024, 259), (4096, 1024, 1024, 258),
+                                           (1000, 768, 3072, 128), (300, 256, 192, 0)])
+def test_gemm_residual_fp16_rounding_bitexact(lib, M, N, K, variant):
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    A = torch.randint(-3, 4, (M, K), device="cuda", generator=g).half()
+    W = torch.randint(-2, 3, (N, K), device="cuda", generator=g).half()
+    bias = torch.randint(-8, 9, (N,), device="cuda", generator=g).float() * 0.25
+    X0 = (torch.randn(M, N, device="cuda", generator=g) * 64).half()
+    t = (A.double() @ W.double().t() + bias.double()).half()   # exact sum, one fp16 rounding
+    ref = X0 + t                                      # torch half add
+    X = X0.clone()
+    _check(lib, lib.miclip_op_gemm(0, A.data_ptr(), W.data_ptr(), bias.data_ptr(), X.data_ptr(),
+                                   M, N, K, 4, 0, variant, _stream()))
+    torch.cuda.synchronize()
+    assert torch.equal(X, ref), f"{(X != ref).sum().item()} elements differ"
