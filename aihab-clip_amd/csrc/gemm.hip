@@ -911,7 +911,10 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
       }
     }
   };
-  auto mfma_q = [&](int qi, int qj) {
+  // FIRST (K-tile 0): the k-step-0 MFMAs take a zero accumulator operand (the
+  // inline constant 0), so a tile needs no 128 v_mov zeroing its accumulators
+  auto mfma_q = [&](int qi, int qj, auto first_c) {
+    constexpr bool FIRST = decltype(first_c)::value;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -919,10 +922,11 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
+          const f32x4 c = (FIRST && s == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[qi][qj][i][j];
           if constexpr (TR)   // C^T = W . A^T: lane (fk, fr) = row fr, columns 4fk .. 4fk+3
-            acc[qi][qj][i][j] = Mfma<T>::m16(bf[s][j], af[s][i], acc[qi][qj][i][j]);
+            acc[qi][qj][i][j] = Mfma<T>::m16(bf[s][j], af[s][i], c);
           else
-            acc[qi][qj][i][j] = Mfma<T>::m16(af[s][i], bf[s][j], acc[qi][qj][i][j]);
+            acc[qi][qj][i][j] = Mfma<T>::m16(af[s][i], bf[s][j], c);
         }
     __builtin_amdgcn_s_setprio(0);
   };
@@ -932,14 +936,6 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
   MICLIP_STAMP_BEGIN;
   if (id < ndp) sources(id, m0, n0, asrc, bsrc);
   for (; id < ndp; id += gridDim.x) {
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (TR) {
       // This tile's epilogue operands (bias, and for the folded LN the column
       // sums and the 256 row statistics) go to LDS by DMA now, one 1-KiB piece
@@ -986,7 +982,7 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
     lds_barrier();
     if (wr == 1) lds_barrier();   // stagger (wave-uniform)
     MICLIP_STAMP(0);              // tile top: K-tile 0/1 staging and its wait
-    for (int t = 0; t < nk; ++t) {
+    auto ktile = [&](int t, auto first_c) {
       const int buf = t & 1;
       const char* sA0 = smem + (buf * 4 + 0) * HALF + aoff;
       const char* sA1 = smem + (buf * 4 + 1) * HALF + aoff;
@@ -1015,10 +1011,12 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
         if (p == 3 && t + 2 < nk) stage(3, t + 2);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         lds_barrier();
-        mfma_q(qi, qj);
+        mfma_q(qi, qj, first_c);
         lds_barrier();
       }
-    }
+    };
+    ktile(0, std::true_type{});   // nk >= 2 (the launcher requires K >= 128)
+    for (int t = 1; t < nk; ++t) ktile(t, std::false_type{});
     if (wr == 0) lds_barrier();   // balance the stagger barrier
     MICLIP_STAMP(1);              // main loop
 
