@@ -356,7 +356,7 @@ __global__ __launch_bounds__(DH == 64 ? 640 : 576) void attention_kernel(
     const T* __restrict__ qkv, T* __restrict__ out, int N, int H, int Npad, int nchunks,
     float qk_scale, int prio) {
   using G = HeadGeom<DH>;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
   char* kimg = smem;                  // [Npad][ROWB/2] T
   char* vimg = smem + Npad * G::ROWB;  // [Npad][ROWB/2] T
 
@@ -365,15 +365,35 @@ __global__ __launch_bounds__(DH == 64 ? 640 : 576) void attention_kernel(
   const int D = H * DH, ld = 3 * D;
   const T* base = qkv + (size_t)b * N * ld + h * DH;
 
-  for (int idx = threadIdx.x; idx < Npad * G::CH; idx += blockDim.x) {
-    const int row = idx / G::CH, c = idx - row * G::CH;
-    i16x8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (row < N && c * 8 < DH) {
-      kv = *(const i16x8*)(base + (size_t)row * ld + D + c * 8);
-      vv = *(const i16x8*)(base + (size_t)row * ld + 2 * D + c * 8);
+  if constexpr (DH == 64) {
+    // K / V images by LDS-DMA, 1-KiB pieces of 8 rows, the swizzle applied to
+    // the SOURCE chunk (as the x8 kernel stages them): every piece is issued
+    // before any wait. (The register path below loaded 2 x 16 B per thread and
+    // waited for them before its next pair -- ~8 serial round trips per head
+    // at N = 577.) Pad rows repeat row N - 1: finite data under masked keys.
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    const int prow = lane >> 3, pch = lane & 7, pieces = Npad / 8;
+    for (int pc = wave; pc < 2 * pieces; pc += nwv) {
+      const bool isv = pc >= pieces;
+      const int piece = isv ? pc - pieces : pc;
+      const int row = piece * 8 + prow;
+      const int r = row < N ? row : N - 1;
+      const int lch = isv ? (pch ^ ((row & 3) << 1)) : (pch ^ ((row >> 1) & 7));
+      glds16_hidden(base + (size_t)r * ld + (isv ? 2 * D : D) + lch * 8,
+                    (isv ? vimg : kimg) + piece * 1024);
     }
-    *(i16x8*)(kimg + row * G::ROWB + (G::swz(c, (row >> 1) & 7) << 4)) = kv;
-    *(i16x8*)(vimg + row * G::ROWB + (G::swz(c, (row & 3) << 1) << 4)) = vv;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    for (int idx = threadIdx.x; idx < Npad * G::CH; idx += blockDim.x) {
+      const int row = idx / G::CH, c = idx - row * G::CH;
+      i16x8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (row < N && c * 8 < DH) {
+        kv = *(const i16x8*)(base + (size_t)row * ld + D + c * 8);
+        vv = *(const i16x8*)(base + (size_t)row * ld + 2 * D + c * 8);
+      }
+      *(i16x8*)(kimg + row * G::ROWB + (G::swz(c, (row >> 1) & 7) << 4)) = kv;
+      *(i16x8*)(vimg + row * G::ROWB + (G::swz(c, (row & 3) << 1) << 4)) = vv;
+    }
   }
   __syncthreads();
 
