@@ -570,8 +570,9 @@ __global__ __launch_bounds__(SPLIT ? 512 : 640) void attention_pipe_kernel(
 // on VALU (attend_extra_keys: no 31/32-masked ninth tile) and, flash-decoding
 // style, key tile w of the ragged last chunk (N - 256 queries: the 257th
 // token; wave 7 also its extra keys); its partial (m, l, o) per valid query
-// goes to LDS and, after the head's closing barrier, wave v merges queries v,
-// v+8, ... in a fixed order.
+// goes to LDS; wave v computes the extra keys' partial of ragged query v before
+// the head's closing barrier and merges the nine partials after it, in a fixed
+// order.
 // ---------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restrict__ qkv,
@@ -605,8 +606,8 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
   for (int j = 0; j < nh; ++j) {
     const int bh = bh0 + j, b = bh / H, h = bh - b * H;
     const T* base = head_base(bh);
-    // every wave finished reading the previous head's K/V and partials (the
-    // closing barrier below) before these DMAs overwrite them
+    // every wave finished reading the previous head's K/V (the closing barrier
+    // below: the extra keys are taken before it) before these DMAs overwrite them
     for (int pc = wave; pc < 2 * pieces; pc += 8) {
       const bool isv = pc >= pieces;
       const int piece = isv ? pc - pieces : pc;
@@ -658,19 +659,17 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
         }
       }
     }
-    MICLIP_STAMP(3);     // ragged chunk's key-tile slice + partial
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    MICLIP_STAMP(4);     // closing barrier
-    // merge the ragged chunk: wave v takes queries v, v+8, ...; lane = output
-    // dim. The keys past the 8 full tiles join as a ninth partial computed here
-    // (lane = dim: the dot product by a wave sum; K / V rows still resident).
-    for (int c = wave; c < nvalid; c += 8) {
-      const float* pc = part + (size_t)c * 66;
-      const float qd = to_f<T>(base[(size_t)(256 + c) * ld + lane]);
-      float me = -1e30f, le = 0.f, oe = 0.f;
+    // The keys past the 8 full tiles join the ragged chunk's query c as a ninth
+    // partial, computed by wave c BEFORE the closing barrier (lane = dim: the dot
+    // product by a wave sum) while this head's K / V rows are still resident:
+    // after that barrier the other waves start the next head's DMA into the same
+    // image, so nothing below the barrier may read kimg / vimg. nvalid <= 3 < 8,
+    // so a wave holds at most one query.
+    float me = -1e30f, le = 0.f, oe = 0.f;
+    if (wave < nvalid) {
+      const float qd = to_f<T>(base[(size_t)(256 + wave) * ld + lane]);
+      const int ch = lane >> 3;
       for (int k = 256; k < N; ++k) {
-        const int ch = (lane >> 3);
         const float kd = to_f<T>(*(const T*)(kimg + k * 128 + ((ch ^ ((k >> 1) & 7)) << 4) + (lane & 7) * 2));
         const float sc = wave_sum(qd * kd) * c2;
         const float mn = fmaxf(me, sc), al = __builtin_amdgcn_exp2f(me - mn);
@@ -680,6 +679,16 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
         oe = oe * al + to_f<T>(to_t<T>(p)) * vd;
         me = mn;
       }
+    }
+    MICLIP_STAMP(3);     // ragged chunk's key-tile slice + partial + extra keys
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    MICLIP_STAMP(4);     // closing barrier
+    // merge the ragged chunk: wave c takes query c; lane = output dim. Reads only
+    // the partials, which the next head's partial writes cannot reach before its
+    // first barrier (every merging wave joins it after the merge).
+    if (wave < nvalid) {
+      const float* pc = part + (size_t)wave * 66;
       float mx = me;
 #pragma unroll
       for (int i = 0; i < 8; ++i) mx = fmaxf(mx, pc[(size_t)i * nvalid * 66 + 64]);
@@ -692,11 +701,9 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
         l += w * pi[65];
         acc += w * pi[lane];
       }
-      obase[(size_t)(256 + c) * D + lane] = to_t<T>(acc / l);
+      obase[(size_t)(256 + wave) * D + lane] = to_t<T>(acc / l);
     }
     MICLIP_STAMP(5);     // merge
-    // the merge's partial reads finish before the next head's partial writes:
-    // those follow the next head's first barrier, which every merging wave joins
   }
   MICLIP_STAMP_END(blockIdx.x * 8 + wave);
 }
@@ -869,7 +876,8 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, 
   // must stay under 80 KiB of LDS, i.e. N - 256 <= 3)
   const size_t lds_x8 = lds + (size_t)8 * (N > 256 ? N - 256 : 0) * 66 * 4;
   if (variant == 8 || (!CAUSAL && variant == 0 && N >= 256 && N < 288 && lds_x8 <= 80 * 1024)) {
-    if (CAUSAL || N < 256 || N >= 288 || lds_x8 > 80 * 1024) return hipErrorInvalidValue;
+    // at most 3 ragged queries: one per merging wave (attention_x8_kernel)
+    if (CAUSAL || N < 256 || N > 259 || lds_x8 > 80 * 1024) return hipErrorInvalidValue;
     static bool x8_attr = false;
     if (!x8_attr) {
       const hipError_t e = hipFuncSetAttribute((const void*)attention_x8_kernel<T>,

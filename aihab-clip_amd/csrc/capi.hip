@@ -494,8 +494,8 @@ bool cls_last_block() {
 }
 
 // encode_image for B images whose workspace window is `w` (clip/model.py:216-235)
-int encode_image_part(miclip_model* m, Workspace w, const float* images, int B, float* out,
-                      uint32_t flags, hipStream_t s) {
+int encode_image_part(miclip_model* m, Workspace w, const void* images, int in_dt, int B,
+                      float* out, uint32_t flags, hipStream_t s) {
   const auto& c = m->cfg;
   const int P = c.vision_patch_size, R = c.image_resolution, W = c.vision_width;
   const int dh = c.vision_head_dim, g = R / P, np = g * g, N = np + 1, H = W / dh;
@@ -503,8 +503,9 @@ int encode_image_part(miclip_model* m, Workspace w, const float* images, int B, 
   const int M = B * N;
   int rc;
   {
-    ProfScope p(m, K_IM2COL, s, 0, (double)B * 3 * R * R * 4 + (double)B * np * m->Kp * 2);
-    MICLIP_HIP(im2col(dt, images, w.patches, B, R, P, m->Kp, s));
+    ProfScope p(m, K_IM2COL, s, 0,
+                (double)B * 3 * R * R * (in_dt == kIn32 ? 4 : 2) + (double)B * np * m->Kp * 2);
+    MICLIP_HIP(im2col(dt, in_dt, images, w.patches, B, R, P, m->Kp, s));
   }
   {
     const double dM = (double)B * np;
@@ -658,6 +659,15 @@ int load_weights(miclip_model* m, const miclip_tensor* t, int32_t n, bool device
     }
     return rc;
   };
+  // HIP errors leave through done() too: it synchronises before freeing the
+  // staging buffer a cast may still be reading
+#define LW_HIP(expr)                                                                   \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess)                                                              \
+      return done(fail(_e == hipErrorInvalidValue ? MICLIP_EINVAL : MICLIP_EHIP,       \
+                       std::string(#expr) + ": " + hipGetErrorString(_e)));           \
+  } while (0)
   for (int i = 0; i < n; ++i) {
     if (!t[i].name || !t[i].data) return done(fail(MICLIP_EINVAL, "null tensor name/data"));
     auto it = m->slots.find(t[i].name);
@@ -671,7 +681,7 @@ int load_weights(miclip_model* m, const miclip_tensor* t, int32_t n, bool device
     int rc;
     if (slot.kind == 0) {
       if (!*slot.dst && (rc = dev_alloc(m, slot.dst, (size_t)slot.numel * 4))) return done(rc);
-      MICLIP_HIP(hipMemcpy(*slot.dst, t[i].data, (size_t)slot.numel * 4, kind));
+      LW_HIP(hipMemcpy(*slot.dst, t[i].data, (size_t)slot.numel * 4, kind));
       slot.loaded = true;
       continue;
     }
@@ -696,14 +706,14 @@ int load_weights(miclip_model* m, const miclip_tensor* t, int32_t n, bool device
     if (!device_src) {
       if (src_bytes > stage_bytes) {
         if (stage) {
-          MICLIP_HIP(hipDeviceSynchronize());
+          LW_HIP(hipDeviceSynchronize());
           dev_free(m, stage);
           stage = nullptr;
         }
         if ((rc = dev_alloc(m, &stage, src_bytes))) return done(rc);
         stage_bytes = src_bytes;
       }
-      MICLIP_HIP(hipMemcpy(stage, t[i].data, src_bytes, hipMemcpyHostToDevice));
+      LW_HIP(hipMemcpy(stage, t[i].data, src_bytes, hipMemcpyHostToDevice));
       src = (const float*)stage;
     }
     if (slot.sdst) {
@@ -711,18 +721,19 @@ int load_weights(miclip_model* m, const miclip_tensor* t, int32_t n, bool device
       const size_t nb = (size_t)rows * cols;
       if (!*slot.dst && (rc = dev_alloc(m, slot.dst, nb))) return done(rc);
       if (!*slot.sdst && (rc = dev_alloc(m, slot.sdst, mx_scale_bytes(rows, cols)))) return done(rc);
-      MICLIP_HIP(quant_mx(0, src, (int)rows, (int)cols, *slot.dst, *slot.sdst, nullptr));
+      LW_HIP(quant_mx(0, src, (int)rows, (int)cols, *slot.dst, *slot.sdst, nullptr));
     } else {
       if (!*slot.dst && (rc = dev_alloc(m, slot.dst, (size_t)rows * cols * elt()))) return done(rc);
-      MICLIP_HIP(cast_pad(m->dtype, src, *slot.dst, rows, (int)src_cols, (int)cols, nullptr));
+      LW_HIP(cast_pad(m->dtype, src, *slot.dst, rows, (int)src_cols, (int)cols, nullptr));
     }
     // the next upload reuses the staging buffer: finish this conversion first
-    if (!device_src) MICLIP_HIP(hipStreamSynchronize(nullptr));
+    if (!device_src) LW_HIP(hipStreamSynchronize(nullptr));
     slot.loaded = true;
   }
-  if (device_src) MICLIP_HIP(hipDeviceSynchronize());
+  if (device_src) LW_HIP(hipDeviceSynchronize());
   return done(0);
 }
+#undef LW_HIP
 
 }  // namespace
 
@@ -763,7 +774,16 @@ static int image_splits(const miclip_model* m, int B, int N) {
 
 int miclip_encode_image(miclip_model* m, const float* images, int32_t B, float* out,
                         uint32_t flags, void* stream) {
+  return miclip_encode_image_ex(m, images, MICLIP_F32, B, out, flags, stream);
+}
+
+int miclip_encode_image_ex(miclip_model* m, const void* images, int32_t image_dtype, int32_t B,
+                           float* out, uint32_t flags, void* stream) {
   if (!m || !images || !out || B < 1) return fail(MICLIP_EINVAL, "bad argument to encode_image");
+  if (image_dtype != MICLIP_F32 && image_dtype != MICLIP_FP16 && image_dtype != MICLIP_BF16)
+    return fail(MICLIP_EINVAL, "image_dtype must be MICLIP_F32, MICLIP_FP16 or MICLIP_BF16");
+  const int in_dt = image_dtype == MICLIP_F32 ? kIn32 : image_dtype == MICLIP_FP16 ? kF16 : kBF16;
+  const size_t in_bytes = image_dtype == MICLIP_F32 ? 4 : 2;
   if (!tower_loaded(m, true))
     return fail(MICLIP_ENOWEIGHTS, "visual weights not loaded (missing " + missing(m, true) + ")");
   if (int rc0 = ensure_folded(m, true)) return rc0;
@@ -780,7 +800,8 @@ int miclip_encode_image(miclip_model* m, const float* images, int32_t B, float* 
   // MFMA-bound GEMMs, and a GEMM's partial last wave of tiles is filled by
   // another stream's work). Each part uses its own window of the workspace.
   const int splits = image_splits(m, B, N);
-  if (splits == 1) return encode_image_part(m, view(m, m->wimg, 0, 0, N, W), images, B, out, flags, s);
+  if (splits == 1)
+    return encode_image_part(m, view(m, m->wimg, 0, 0, N, W), images, in_dt, B, out, flags, s);
   if ((rc = ensure_aux(m, splits - 1))) return rc;
   MICLIP_HIP(hipEventRecord(m->ev_fork, s));
   int b0 = 0;
@@ -789,8 +810,8 @@ int miclip_encode_image(miclip_model* m, const float* images, int32_t B, float* 
     hipStream_t sp = p == 0 ? s : m->aux[p - 1];
     if (p > 0) MICLIP_HIP(hipStreamWaitEvent(sp, m->ev_fork, 0));
     if ((rc = encode_image_part(m, view(m, m->wimg, (size_t)b0 * N, b0, N, W, p),
-                                images + (size_t)b0 * 3 * R * R, nb, out + (size_t)b0 * dim,
-                                flags, sp)))
+                                (const char*)images + (size_t)b0 * 3 * R * R * in_bytes, in_dt,
+                                nb, out + (size_t)b0 * dim, flags, sp)))
       return rc;
     b0 += nb;
   }
@@ -877,6 +898,12 @@ int miclip_preprocess(miclip_model* m, const uint8_t* pixels, const miclip_image
   if (e != hipSuccess)
     return fail(e == hipErrorInvalidValue ? MICLIP_EINVAL : MICLIP_EHIP,
                 err[0] ? std::string(err) : std::string("preprocess: ") + hipGetErrorString(e));
+  return 0;
+}
+
+int miclip_clock_probe(uint64_t* out, int32_t n_wg, void* stream) {
+  if (!out || n_wg < 1 || n_wg > 4096) return fail(MICLIP_EINVAL, "bad argument to clock_probe");
+  MICLIP_HIP(clock_probe((unsigned long long*)out, n_wg, (hipStream_t)stream));
   return 0;
 }
 

@@ -78,6 +78,8 @@ __host__ __device__ inline size_t mx_scale_index(int r, int kb, int KT) {
 namespace miclip {
 
 enum DType { kF16 = 0, kBF16 = 1 };
+// image input element type of encode_image_ex (MICLIP_F32 in include/miclip.h)
+constexpr int kIn32 = 3;
 
 template <typename T> struct Mfma;
 

@@ -16,8 +16,9 @@ namespace miclip {
 
 namespace {
 
-template <typename T>
-__global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ img,
+// I: image element type (fp32, or fp16 / bf16 device-resident input batches)
+template <typename T, typename I>
+__global__ __launch_bounds__(256) void im2col_kernel(const I* __restrict__ img,
                                                      T* __restrict__ patches, int R, int P,
                                                      int Kp) {
   const int g = R / P, np = g * g;
@@ -25,16 +26,35 @@ __global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ i
   const int b = row / np, pi = row - b * np;
   const int py = pi / g, px = pi - py * g;
   const int PP = P * P, K = 3 * PP;
-  const float* src = img + (size_t)b * 3 * R * R + (size_t)(py * P) * R + px * P;
+  const I* src = img + (size_t)b * 3 * R * R + (size_t)(py * P) * R + px * P;
   T* dst = patches + (size_t)row * Kp;
   for (int col = threadIdx.x; col < Kp; col += blockDim.x) {
     float v = 0.f;
     if (col < K) {
       const int c = col / PP, rem = col - c * PP;
       const int ky = rem / P, kx = rem - ky * P;
-      v = src[(size_t)c * R * R + ky * R + kx];
+      v = to_f<I>(src[(size_t)c * R * R + ky * R + kx]);
     }
     dst[col] = to_t<T>(v);
+  }
+}
+
+// One wave per workgroup: which XCD it runs on, the shader-clock counter
+// (s_memtime: free-running at the core clock) and the 100 MHz real-time
+// counter. bench.py launches it on the timed stream before and after the timed
+// steps; per XCD, delta(s_memtime) / delta(s_memrealtime) x 100 MHz is the
+// clock the chip held over the steps. Lane 0 stores (vector stores).
+__global__ __launch_bounds__(64) void clock_probe_kernel(unsigned long long* __restrict__ out) {
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+  const unsigned long long r = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    unsigned long long* o = out + 4 * (size_t)blockIdx.x;
+    o[0] = xcc & 0xfu;
+    o[1] = t;
+    o[2] = r;
+    o[3] = 0;
   }
 }
 
@@ -303,17 +323,35 @@ hipError_t row_l2norm(float* x, int R, int D, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t im2col(int dtype, const float* img, void* patches, int B, int R, int P, int Kp,
-                  hipStream_t s) {
-  if (B < 1 || P < 1 || R % P || Kp < 3 * P * P) return hipErrorInvalidValue;
+template <typename T>
+static hipError_t im2col_t(int in_dtype, const void* img, T* patches, int B, int R, int P, int Kp,
+                           hipStream_t s) {
   const int np = (R / P) * (R / P);
-  if (dtype == kF16)
-    hipLaunchKernelGGL(im2col_kernel<_Float16>, dim3(B * np), dim3(256), 0, s, img,
-                       (_Float16*)patches, R, P, Kp);
+  if (in_dtype == kIn32)
+    hipLaunchKernelGGL((im2col_kernel<T, float>), dim3(B * np), dim3(256), 0, s,
+                       (const float*)img, patches, R, P, Kp);
+  else if (in_dtype == kF16)
+    hipLaunchKernelGGL((im2col_kernel<T, _Float16>), dim3(B * np), dim3(256), 0, s,
+                       (const _Float16*)img, patches, R, P, Kp);
+  else if (in_dtype == kBF16)
+    hipLaunchKernelGGL((im2col_kernel<T, __bf16>), dim3(B * np), dim3(256), 0, s,
+                       (const __bf16*)img, patches, R, P, Kp);
   else
-    hipLaunchKernelGGL(im2col_kernel<__bf16>, dim3(B * np), dim3(256), 0, s, img,
-                       (__bf16*)patches, R, P, Kp);
+    return hipErrorInvalidValue;
   return hipGetLastError();
+}
+
+hipError_t clock_probe(unsigned long long* out, int n_wg, hipStream_t s) {
+  if (!out || n_wg < 1 || n_wg > 4096) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(clock_probe_kernel, dim3(n_wg), dim3(64), 0, s, out);
+  return hipGetLastError();
+}
+
+hipError_t im2col(int dtype, int in_dtype, const void* img, void* patches, int B, int R, int P,
+                  int Kp, hipStream_t s) {
+  if (B < 1 || P < 1 || R % P || Kp < 3 * P * P) return hipErrorInvalidValue;
+  if (dtype == kF16) return im2col_t(in_dtype, img, (_Float16*)patches, B, R, P, Kp, s);
+  return im2col_t(in_dtype, img, (__bf16*)patches, B, R, P, Kp, s);
 }
 
 hipError_t class_token(const float* cls, const float* pos, void* X, int B, int ntok, int D,

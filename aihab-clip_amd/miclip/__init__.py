@@ -13,7 +13,8 @@ import warnings
 
 import torch
 
-from .configs import MODEL_CONFIGS, CLIPConfig, available_models, config_from_state_dict
+from .configs import (MODEL_CONFIGS, OPEN_CLIP_MODELS, CLIPConfig, available_models,
+                      config_from_state_dict)
 from .model import CLIP, build_model
 from .preprocess import Transform
 from .weights import generate_state_dict, synthetic_images
@@ -27,7 +28,7 @@ def _transform(n_px):
 
 
 def load(name, device="cuda" if torch.cuda.is_available() else "cpu", jit=False,
-         download_root=None, *, seed: int = 0, compute_dtype: str = "fp16"):
+         download_root=None, *, seed: int = 0, compute_dtype: str = "fp16", surface=None):
     """Counterpart of clip.load (clip/clip.py:89-137): returns (state_dict, model, preprocess).
 
     `name` is a model name from available_models() -- resolved offline to the
@@ -36,7 +37,13 @@ def load(name, device="cuda" if torch.cuda.is_available() else "cpu", jit=False,
     else raises RuntimeError like the reference. `jit=True` is accepted with a
     warning and loads the non-JIT model (the reference does the same when the
     file is not a JIT archive, clip/clip.py:127-130). `download_root` is unused.
+    `surface` picks the model's call contract: "openai" (the vendored
+    clip/model.py: pre-projection encode_image, tuple encode_text) or
+    "open_clip" (post-projection, one tensor; methods/PEFT_openclip.py); it
+    defaults to "open_clip" for open_clip model names (OPEN_CLIP_MODELS).
     """
+    if surface is None:
+        surface = "open_clip" if name in OPEN_CLIP_MODELS else "openai"
     if name in MODEL_CONFIGS:
         cfg = MODEL_CONFIGS[name]
         sd = generate_state_dict(cfg, seed=seed)
@@ -52,7 +59,7 @@ def load(name, device="cuda" if torch.cuda.is_available() else "cpu", jit=False,
         raise RuntimeError(f"Model {name} not found; available models = {available_models()}")
     if jit:
         warnings.warn(f"{name}: JIT archives are not supported by miclip; loading as a state dict")
-    model = CLIP(cfg, sd, device=device, compute_dtype=compute_dtype).eval()
+    model = CLIP(cfg, sd, device=device, compute_dtype=compute_dtype, surface=surface).eval()
     return model.state_dict(), model, _transform(cfg.image_resolution)
 
 

@@ -10,10 +10,11 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MICLIP_LIB", os.path.join(_HERE, "libmiclip.so"))
 
-ABI_VERSION = 5          # include/miclip.h MICLIP_ABI_VERSION
+ABI_VERSION = 6          # include/miclip.h MICLIP_ABI_VERSION
 MICLIP_FP16 = 0
 MICLIP_BF16 = 1
 MICLIP_MXFP8 = 2
+MICLIP_F32 = 3
 MICLIP_ACT_QUICKGELU = 1
 MICLIP_ACT_GELU = 2
 MICLIP_FLAG_NORMALIZE = 1
@@ -25,7 +26,8 @@ MICLIP_MODEL_MXFP8 = 4
 EXPORTS = (
     "miclip_model_create", "miclip_model_load_weights", "miclip_model_load_weights_device",
     "miclip_reserve",
-    "miclip_encode_image", "miclip_encode_text", "miclip_zero_shot",
+    "miclip_encode_image", "miclip_encode_image_ex", "miclip_encode_text", "miclip_zero_shot",
+    "miclip_clock_probe",
     "miclip_model_destroy", "miclip_last_error", "miclip_abi_version",
     "miclip_model_bytes", "miclip_model_flags", "miclip_set_profiling", "miclip_profile_read", "miclip_set_splits", "miclip_image_splits",
     "miclip_op_gemm", "miclip_op_ln_stats", "miclip_op_ln_fold", "miclip_op_gemm_ln",
@@ -84,6 +86,8 @@ def load_library(path: str = None):
         "miclip_model_load_weights_device": ([vp, ctypes.POINTER(MiclipTensor), i32], ctypes.c_int),
         "miclip_reserve": ([vp, i32, i32], ctypes.c_int),
         "miclip_encode_image": ([vp, vp, i32, vp, u32, vp], ctypes.c_int),
+        "miclip_encode_image_ex": ([vp, vp, i32, i32, vp, u32, vp], ctypes.c_int),
+        "miclip_clock_probe": ([vp, i32, vp], ctypes.c_int),
         "miclip_encode_text": ([vp, vp, i32, vp, vp, vp], ctypes.c_int),
         "miclip_zero_shot": ([vp, vp, i32, i32, vp, i32, f32, vp, vp, i32, vp], ctypes.c_int),
         "miclip_model_destroy": ([vp], None),

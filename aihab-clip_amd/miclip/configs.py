@@ -76,6 +76,11 @@ MODEL_CONFIGS = {
 }
 
 
+# Names whose reference loader is open_clip (aihab_utils/model_init.py:42-112), so
+# miclip.load gives them open_clip's model surface by default (model.py).
+OPEN_CLIP_MODELS = frozenset({"ViT-H-14"})
+
+
 def available_models():
     """Counterpart of clip.available_models (clip/clip.py:84-86), ViT names only."""
     return list(MODEL_CONFIGS.keys())
@@ -119,3 +124,18 @@ def algorithmic_gflop_per_image(cfg: CLIPConfig) -> float:
     W, L, N, P = cfg.vision_width, cfg.vision_layers, cfg.n_tokens, cfg.vision_patch_size
     n = N - 1
     return (2 * n * 3 * P * P * W + L * (24 * N * W * W + 4 * N * N * W)) / 1e9
+
+
+def executed_gflop_per_image(cfg: CLIPConfig, cls_last: bool = True) -> float:
+    """FLOPs encode_image's kernels execute per image. With the last vision block
+    on the CLS rows only (capi.hip run_block(cls_only), default; its other rows
+    never reach ln_post(x[:, 0, :]), clip/model.py:226-229) that block runs its QKV
+    GEMM over all N rows (keys / values) but attention for one query and
+    out-proj + MLP on one row: 6NW^2 + 4NW + 18W^2 instead of 24NW^2 + 4N^2W."""
+    full = algorithmic_gflop_per_image(cfg)
+    if not cls_last:
+        return full
+    W, N = cfg.vision_width, cfg.n_tokens
+    layer = 24 * N * W * W + 4 * N * N * W
+    last = 6 * N * W * W + 4 * N * W + 18 * W * W
+    return full - (layer - last) / 1e9

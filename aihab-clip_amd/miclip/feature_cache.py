@@ -19,7 +19,9 @@ and the multi-GPU variant:
     encodes a contiguous slice of the image batch and the L2-normalised (or
     raw) embeddings are all-gathered over RCCL (torch.distributed backend
     "nccl" on ROCm) back into the single-GPU row order, so cached
-    embeddings.pt rows still line up with labels.pt / metadata.csv.
+    embeddings.pt rows still line up with labels.pt / metadata.csv;
+  * ShardedBatchLoader / gather_shards (per_rank=True): each rank reads and
+    decodes only its own slice of every global batch.
 
 Differences that matter to callers: features are fp32 (the reference's GPU
 path returns fp16); the encode itself runs in the C ABI, with the optional
@@ -318,10 +320,7 @@ def sharded_encode(encode_fn, images, group=None, dim: Optional[int] = None):
     width = dim if dim is not None else (local.shape[1] if local is not None else None)
     if width is None:
         raise ValueError("sharded_encode needs `dim` when a rank has an empty shard")
-    if dist.get_backend(group) == "nccl":
-        dev = torch.device("cuda", torch.cuda.current_device())
-    else:
-        dev = torch.device("cpu")
+    dev = _collective_device(group)
     per = -(-n // world)
     if (local is not None and hi - lo == per and local.device == dev
             and local.dtype == torch.float32 and local.is_contiguous()):
@@ -338,19 +337,108 @@ def sharded_encode(encode_fn, images, group=None, dim: Optional[int] = None):
     return out if local is None else out.to(local.device)
 
 
+def _collective_device(group):
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
 @torch.no_grad()
-def compute_image_features_sharded(clip_model, loader, normalize: bool = True, group=None):
-    """compute_image_features over an image-batch-sharded node: every rank walks the
-    same loader, encodes its slice of each batch on its own GPU and receives the
-    all-gathered (normalised) embeddings; returns (features, labels) on the
-    rank's device in the single-GPU row order."""
+def gather_shards(local, group=None, width: Optional[int] = None, dtype=torch.float32):
+    """All-gather per-rank row blocks of possibly different lengths, in rank order.
+
+    For loaders that hand each rank only its own contiguous slice of a global
+    batch (ShardedBatchLoader): the ranks exchange their row counts (one tiny
+    all-gather), pad to the longest, all-gather, and drop the padding, so the
+    result is the global batch in its original order when rank r holds the r-th
+    slice. `local` may be None (an empty shard); then `width` (columns, 0 for a
+    1-D block such as labels) is required. Without a process group: `local`."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return local
+    world = dist.get_world_size(group)
+    dev = _collective_device(group)
+    n_local = 0 if local is None else int(local.shape[0])
+    if local is not None:
+        width = int(local.shape[1]) if local.dim() == 2 else 0
+        dtype = local.dtype
+    if width is None:
+        raise ValueError("gather_shards needs `width` when a rank has an empty shard")
+    counts = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(counts, torch.tensor([n_local], dtype=torch.int64, device=dev),
+                                group=group)
+    counts = counts.tolist()
+    per = max(counts)
+    shape = (per, width) if width else (per,)
+    buf = torch.zeros(shape, dtype=dtype, device=dev)
+    if n_local:
+        buf[:n_local] = local.to(dev)
+    out = torch.empty((world * per,) + shape[1:], dtype=dtype, device=dev)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    out = torch.cat([out[r * per: r * per + c] for r, c in enumerate(counts)])
+    return out if local is None else out.to(local.device)
+
+
+class ShardedBatchLoader:
+    """Per-rank loader: global batch b covers dataset items [b*bs, min(n, (b+1)*bs));
+    this rank reads and decodes only its contiguous slice shard_range(len, rank,
+    world) of it, so no rank touches the other ranks' images (the reference's
+    DataLoader, aihab_utils/feature_cache.py:114-142, decodes the whole batch).
+    Yields (images, targets) from `collate_fn` over (image, target) items, or
+    (None, empty targets) when the slice is empty (a last batch smaller than the
+    world). compute_image_features_sharded(..., per_rank=True) restores the
+    global order with gather_shards."""
+
+    def __init__(self, dataset, batch_size: int, rank: Optional[int] = None,
+                 world: Optional[int] = None, collate_fn=None):
+        self.dataset = dataset
+        self.batch_size = int(batch_size)
+        init = dist.is_available() and dist.is_initialized()
+        self.rank = rank if rank is not None else (dist.get_rank() if init else 0)
+        self.world = world if world is not None else (dist.get_world_size() if init else 1)
+        self.collate_fn = collate_fn or self._stack
+
+    @staticmethod
+    def _stack(items):
+        imgs = [i[0] if isinstance(i[0], torch.Tensor) else torch.as_tensor(i[0]) for i in items]
+        return torch.stack(imgs), torch.as_tensor([int(i[1]) for i in items], dtype=torch.int64)
+
+    def __len__(self):
+        return -(-len(self.dataset) // self.batch_size)
+
+    def __iter__(self):
+        n = len(self.dataset)
+        for b0 in range(0, n, self.batch_size):
+            nb = min(self.batch_size, n - b0)
+            lo, hi = shard_range(nb, self.rank, self.world)
+            if hi > lo:
+                yield self.collate_fn([self.dataset[b0 + i] for i in range(lo, hi)])
+            else:
+                yield None, torch.empty(0, dtype=torch.int64)
+
+
+@torch.no_grad()
+def compute_image_features_sharded(clip_model, loader, normalize: bool = True, group=None,
+                                   per_rank: bool = False):
+    """compute_image_features over an image-batch-sharded node; returns (features,
+    labels) on the rank's device in the single-GPU row order.
+
+    per_rank=False: every rank walks the same loader, encodes its slice of each
+    batch (sharded_encode) and receives the all-gathered (normalised) embeddings.
+    per_rank=True: the loader yields only this rank's slice of each global batch
+    (ShardedBatchLoader: each rank reads and decodes only its own images); the
+    features and the labels are gathered back into global order (gather_shards)."""
     device = _model_device(clip_model)
-    dim = clip_model.config.vision_width
+    dim = getattr(clip_model, "image_dim", None) or clip_model.config.vision_width
 
     def enc(x):
         return clip_model.encode_image(prepare_images(clip_model, x, device), normalize=normalize)
     feats, labels = [], []
     for images, target in loader:
-        feats.append(sharded_encode(enc, images, group=group, dim=dim))
-        labels.append(target.to(device))
+        if per_rank:
+            local = enc(images) if images is not None and len(images) else None
+            feats.append(gather_shards(local, group=group, width=dim).to(device))
+            labels.append(gather_shards(target.to(torch.int64), group=group, width=0).to(device))
+        else:
+            feats.append(sharded_encode(enc, images, group=group, dim=dim))
+            labels.append(target.to(device))
     return torch.cat(feats), torch.cat(labels)

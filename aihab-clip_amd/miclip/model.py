@@ -16,6 +16,14 @@ touch, and how it is honoured here:
     (clip/model.py:338-353). Outputs are fresh, writable fp32 tensors (callers
     divide them in place, utils.py:46-48).
 
+`surface="open_clip"` (the default for open_clip model names such as
+"ViT-H-14") gives the same graph open_clip's model surface
+instead, the one the PEFT_openclip path calls (methods/PEFT_openclip.py:38-47,
+90-92; aihab_utils/feature_cache.py:124-128): `encode_image(image,
+normalize=False) -> Tensor[B, embed_dim]` post-projection and
+`encode_text(text, normalize=False) -> Tensor[P, embed_dim]` (one tensor), and
+`forward` returns open_clip's (image_features, text_features, logit_scale.exp()).
+
 The encoders never run in PyTorch: they call the C ABI, which fails loudly if
 the library or the device is missing. The Parameters are the source of truth
 for `state_dict`; the handle holds repacked device copies (GEMM weights in the
@@ -26,6 +34,7 @@ import warnings
 
 import numpy as np
 import torch
+import torch.nn.functional as F
 from torch import nn
 
 from . import _lib
@@ -101,11 +110,18 @@ class _Handle:
             pass
 
 
+SURFACES = ("openai", "open_clip")
+
+
 class CLIP(nn.Module):
-    def __init__(self, cfg: CLIPConfig, state_dict, device="cuda", compute_dtype="fp16"):
+    def __init__(self, cfg: CLIPConfig, state_dict, device="cuda", compute_dtype="fp16",
+                 surface="openai"):
         super().__init__()
         if compute_dtype not in _DTYPES:
             raise ValueError(f"compute_dtype must be one of {sorted(_DTYPES)}")
+        if surface not in SURFACES:
+            raise ValueError(f"surface must be one of {SURFACES}")
+        self.surface = surface
         self.config = cfg
         self.compute_dtype = compute_dtype
         self.context_length = cfg.context_length
@@ -170,6 +186,12 @@ class CLIP(nn.Module):
     def device(self):
         return self.visual.conv1.weight.device
 
+    @property
+    def image_dim(self):
+        """Width of encode_image's output: vision_width (OpenAI surface, pre-projection)
+        or embed_dim (open_clip surface, post-projection)."""
+        return self.config.embed_dim if self.surface == "open_clip" else self.config.vision_width
+
     def _require(self):
         if self._handle is None:
             raise RuntimeError("model is not on a HIP device; call .cuda() / .to('cuda')")
@@ -215,19 +237,30 @@ class CLIP(nn.Module):
                 for i in range(n) if arr[i].launches}
 
     @torch.no_grad()
-    def encode_image(self, image, normalize=False, apply_proj=False, out=None):
-        """Pre-projection image features [B, vision_width] (clip/model.py:335-336, 216-235).
+    def encode_image(self, image, normalize=False, apply_proj=None, out=None):
+        """Pre-projection image features [B, vision_width] (clip/model.py:335-336, 216-235);
+        post-projection [B, embed_dim] on the open_clip surface (open_clip's
+        `encode_image(image, normalize=False)`, methods/PEFT_openclip.py:90-92).
 
         normalize / apply_proj fuse the callers' F.normalize
         (aihab_utils/feature_cache.py:126-127) and `@ visual.proj`
-        (methods/ProLIP.py:38-41) into the same launch sequence.
+        (methods/ProLIP.py:38-41) into the same launch sequence; apply_proj
+        defaults to the surface's contract.
         """
         h = self._require()
+        if apply_proj is None:
+            apply_proj = self.surface == "open_clip"
         if image.dim() != 4 or image.shape[1] != 3 or image.shape[2] != image.shape[3] \
                 or image.shape[2] != self.config.image_resolution:
             raise ValueError(f"expected images [B, 3, {self.config.image_resolution}, "
                              f"{self.config.image_resolution}], got {tuple(image.shape)}")
-        img = image.to(device=self.device, dtype=torch.float32).contiguous()
+        # fp16 / bf16 batches are read as they are (miclip_encode_image_ex): the
+        # patchify rounds pixels to the compute dtype anyway, so a half batch in
+        # the compute dtype gives the fp32 batch's features bit for bit
+        in_dt = {torch.float16: _lib.MICLIP_FP16, torch.bfloat16: _lib.MICLIP_BF16}.get(
+            image.dtype, _lib.MICLIP_F32)
+        img = image.to(device=self.device,
+                       dtype=image.dtype if in_dt != _lib.MICLIP_F32 else torch.float32).contiguous()
         B = img.shape[0]
         dim = self.config.embed_dim if apply_proj else self.config.vision_width
         if out is None:
@@ -240,9 +273,9 @@ class CLIP(nn.Module):
         flags = (_lib.MICLIP_FLAG_NORMALIZE if normalize else 0) | \
                 (_lib.MICLIP_FLAG_APPLY_PROJ if apply_proj else 0)
         with torch.cuda.device(self.device):
-            _lib.check(h.lib.miclip_encode_image(h.ptr, img.data_ptr(), B, out.data_ptr(), flags,
-                                                 _lib.stream_handle(self.device)),
-                       "miclip_encode_image")
+            _lib.check(h.lib.miclip_encode_image_ex(h.ptr, img.data_ptr(), in_dt, B, out.data_ptr(),
+                                                    flags, _lib.stream_handle(self.device)),
+                       "miclip_encode_image_ex")
         return out
 
     @torch.no_grad()
@@ -301,8 +334,17 @@ class CLIP(nn.Module):
         return out
 
     @torch.no_grad()
-    def encode_text(self, text):
-        """(x_before_proj [P, transformer_width], x [P, embed_dim]) (clip/model.py:338-353)."""
+    def encode_text(self, text, normalize=False):
+        """(x_before_proj [P, transformer_width], x [P, embed_dim]) (clip/model.py:338-353);
+        on the open_clip surface one tensor x [P, embed_dim], L2-normalised with
+        normalize=True (open_clip's `encode_text(text, normalize=False)`,
+        methods/PEFT_openclip.py:38-47)."""
+        xb, xp = self._encode_text(text)
+        if normalize:
+            xp = F.normalize(xp, dim=-1)
+        return xp if self.surface == "open_clip" else (xb, xp)
+
+    def _encode_text(self, text):
         h = self._require()
         if text.dim() != 2 or text.shape[1] != self.context_length:
             raise ValueError(f"expected tokens [P, {self.context_length}], got {tuple(text.shape)}")
@@ -352,9 +394,13 @@ class CLIP(nn.Module):
 
         The vendored forward raises (encode_text returns a tuple, SURVEY §0 item 2);
         this one computes what it was meant to: cosine logits with logit_scale.exp().
+        On the open_clip surface: open_clip's (image_features, text_features,
+        logit_scale.exp()), both feature sets L2-normalised.
         """
         img = self.encode_image(image, normalize=True, apply_proj=True)
-        _, txt = self.encode_text(text)
+        _, txt = self._encode_text(text)
+        if self.surface == "open_clip":
+            return img, F.normalize(txt, dim=-1), self.logit_scale.exp()
         txt = txt / txt.norm(dim=-1, keepdim=True)
         logits_per_image = self.logit_scale.exp() * img @ txt.t()
         return logits_per_image, logits_per_image.t()
@@ -363,10 +409,10 @@ class CLIP(nn.Module):
         c = self.config
         return (f"vision=ViT(W={c.vision_width}, L={c.vision_layers}, P={c.vision_patch_size}, "
                 f"R={c.image_resolution}), text=(W={c.transformer_width}, L={c.transformer_layers}), "
-                f"embed_dim={c.embed_dim}, compute_dtype={self.compute_dtype}")
+                f"embed_dim={c.embed_dim}, compute_dtype={self.compute_dtype}, surface={self.surface}")
 
 
-def build_model(state_dict, device="cuda", compute_dtype="fp16") -> CLIP:
+def build_model(state_dict, device="cuda", compute_dtype="fp16", surface="openai") -> CLIP:
     """Counterpart of reference build_model (clip/model.py:396-433), ViT only."""
     from .configs import config_from_state_dict
     sd = dict(state_dict)
@@ -376,4 +422,4 @@ def build_model(state_dict, device="cuda", compute_dtype="fp16") -> CLIP:
     if "logit_scale" not in sd:
         warnings.warn("state_dict has no logit_scale; using log(1/0.07)")
         sd["logit_scale"] = torch.tensor(float(np.log(1 / 0.07)))
-    return CLIP(cfg, sd, device=device, compute_dtype=compute_dtype).eval()
+    return CLIP(cfg, sd, device=device, compute_dtype=compute_dtype, surface=surface).eval()

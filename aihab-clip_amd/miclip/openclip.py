@@ -1,0 +1,66 @@
+"""open_clip entry points the reference's open_clip path calls, on the HIP model.
+
+aihab_utils/model_init.py:42-112 loads the PEFT_openclip backbone with
+`open_clip.create_model_and_transforms(backbone, pretrained=..., device=...)`
+and tokenises with `open_clip.get_tokenizer(backbone)`; methods/PEFT_openclip.py
+then calls `model.encode_image(images)` (post-projection, :90-92) and
+`model.encode_text(tokens)` (one tensor, :38-47). open_clip itself is not in
+this image and the reference pins no version of it, so what is restated here is
+the contract those call sites use, on miclip's open_clip surface
+(`CLIP(surface="open_clip")`, model.py) -- parity unpinned with respect to
+open_clip's own code.
+
+  * create_model_and_transforms -> (model, preprocess_train, preprocess_val):
+    seeded weights of the named shape (no checkpoints offline), or a state-dict
+    file for `pretrained`; both transforms are the eval transform (Resize
+    bicubic + CenterCrop + CLIP normalise, open_clip's default for the OpenAI
+    mean/std): the training-time augmentation is outside the encode path.
+  * get_tokenizer(name) -> callable(texts, context_length=77): the CLIP BPE
+    (open_clip's SimpleTokenizer is the same vocabulary and padding).
+"""
+import os
+
+import torch
+
+from .configs import OPEN_CLIP_MODELS
+
+
+def list_models():
+    return sorted(OPEN_CLIP_MODELS)
+
+
+def create_model(model_name, pretrained=None, device="cuda", *, compute_dtype="fp16", seed=0,
+                 **_unused):
+    from . import load
+    src = pretrained if pretrained and os.path.isfile(str(pretrained)) else model_name
+    if src == model_name and model_name not in OPEN_CLIP_MODELS:
+        raise RuntimeError(f"Model config for {model_name} not found; available models "
+                           f"{list_models()}.")
+    _, model, _ = load(src, device=device, compute_dtype=compute_dtype, seed=seed,
+                       surface="open_clip")
+    return model
+
+
+def create_model_and_transforms(model_name, pretrained=None, device="cuda", *,
+                                compute_dtype="fp16", seed=0, **kwargs):
+    from . import _transform
+    model = create_model(model_name, pretrained, device, compute_dtype=compute_dtype, seed=seed,
+                         **kwargs)
+    pre = _transform(model.config.image_resolution)
+    return model, pre, pre
+
+
+def get_tokenizer(model_name=None):
+    from . import tokenize
+
+    def tok(texts, context_length: int = 77):
+        # open_clip's tokenizer truncates over-long prompts (keeping the EOT token)
+        return tokenize(texts, context_length=context_length, truncate=True)
+    return tok
+
+
+@torch.no_grad()
+def encode_image_features(model, images, normalize=True):
+    """What aihab_utils/feature_cache.py:124-128 stores per batch: post-projection
+    (open_clip surface) embeddings, L2-normalised when asked, normalise fused."""
+    return model.encode_image(images, normalize=normalize, apply_proj=True)

@@ -1,0 +1,8 @@
+"""`import open_clip` drop-in for the reference's open_clip path
+(aihab_utils/model_init.py:42-112, methods/PEFT_openclip.py): with
+`aihab-clip_amd/` first on sys.path, `open_clip.create_model_and_transforms`,
+`open_clip.get_tokenizer` and `open_clip.create_model` resolve to miclip's
+MI355X encode path (open_clip model surface)."""
+from miclip.openclip import create_model, create_model_and_transforms, get_tokenizer, list_models  # noqa: F401
+
+__all__ = ["create_model", "create_model_and_transforms", "get_tokenizer", "list_models"]

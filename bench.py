@@ -167,25 +167,84 @@ def attach_traffic(model_name, dtype, epi, M):
 
 # --------------------------------------------------------------------- rank --
 
-def run(args):
+def _load_miclip(name, dev, dtype):
+    import miclip
+    # OpenAI surface for every model (pre-projection encode, projection in the head)
+    _, model, _ = miclip.load(name, device=dev, compute_dtype=dtype, surface="openai")
+    return model
+
+
+class ClockProbe:
+    """Core clock the chip held over a timed region (miclip_clock_probe): one-wave
+    workgroups on the timed stream read s_memtime (shader-clock counter) and
+    s_memrealtime (100 MHz) before and after; per XCD (HW_REG_XCC_ID)
+    delta(memtime) / delta(realtime) x 100 MHz, median over the XCDs."""
+
+    NWG = 64          # 8 per XCD under round-robin dispatch
+
+    def __init__(self, dev):
+        import torch
+        from miclip import _lib
+        self.lib = _lib.load_library()
+        self.torch = torch
+        self.dev = dev
+        self.buf = torch.zeros(2, self.NWG, 4, dtype=torch.int64, device=dev)
+
+    def mark(self, i):
+        from miclip import _lib
+        _lib.check(self.lib.miclip_clock_probe(self.buf[i].data_ptr(), self.NWG,
+                                               _lib.stream_handle(self.dev)), "miclip_clock_probe")
+
+    def ghz(self):
+        import numpy as np
+        b = self.buf.cpu().numpy()
+        per_xcd = {}
+        for x in np.unique(b[0, :, 0]):
+            a0, a1 = b[0][b[0, :, 0] == x], b[1][b[1, :, 0] == x]
+            if len(a0) == 0 or len(a1) == 0:
+                continue
+            dt = float(np.median(a1[:, 1]) - np.median(a0[:, 1]))
+            dr = float(np.median(a1[:, 2]) - np.median(a0[:, 2]))
+            if dr > 0:
+                per_xcd[int(x)] = dt / dr * 0.1        # GHz (realtime ticks at 100 MHz)
+        if not per_xcd:
+            return None, {}
+        vals = sorted(per_xcd.values())
+        return round(float(np.median(vals)), 4), {k: round(v, 4) for k, v in sorted(per_xcd.items())}
+
+
+def run(args, backend="nccl", load_model=None):
+    """One rank of the bench. backend "nccl" (RCCL, the product) on the rank's HIP
+    device; "gloo" runs the same rank logic on the host (tests/test_bench_ranks.py
+    drives it at world 2 with a stub model). Returns rank 0's JSON line (dict)."""
     import torch
     import torch.distributed as dist
 
+    on_gpu = backend == "nccl"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-        world = dist.get_world_size()            # the group RCCL actually formed
+        if on_gpu:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
+        world = dist.get_world_size()            # the group the backend actually formed
         rank = dist.get_rank()
     if args.gpus != world and rank == 0:
         log(f"[bench] --gpus {args.gpus} but the process group has {world} ranks; reporting {world}")
-    torch.cuda.set_device(local)
-    dev = torch.device(f"cuda:{local}")
+    if on_gpu:
+        torch.cuda.set_device(local)
+        dev = torch.device(f"cuda:{local}")
+    else:
+        dev = torch.device("cpu")
 
-    import miclip
-    from miclip.configs import MODEL_CONFIGS, algorithmic_gflop_per_image
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+
+    from miclip.configs import MODEL_CONFIGS, algorithmic_gflop_per_image, executed_gflop_per_image
     from miclip.feature_cache import shard_range, sharded_encode
     from miclip.weights import CLIP_MEAN, CLIP_STD
     cfg = MODEL_CONFIGS[args.model]
@@ -193,7 +252,8 @@ def run(args):
     n_global = args.batch * world if args.scaling == "weak" else args.batch
     lo, hi = shard_range(n_global, rank, world)
     t_load = time.perf_counter()
-    _, model, _ = miclip.load(args.model, device=dev, compute_dtype=args.dtype)
+    load_model = load_model or _load_miclip
+    model = load_model(args.model, dev, args.dtype)
     peak = PEAK_TFLOPS * (2 if args.dtype == "mxfp8" else 1)   # MX-fp8 runs at 2x the f16 rate
     model.reserve(max(hi - lo, 1), args.classes)
     model.set_splits(args.splits)
@@ -234,15 +294,19 @@ def run(args):
 
     step = make_step(model)
 
-    def timed(fn, steps):
-        torch.cuda.synchronize()
+    def timed(fn, steps, clock=None):
+        sync()
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        sync()
         t0 = time.perf_counter()
+        if clock is not None:
+            clock.mark(0)
         for _ in range(steps):
             fn()
-        torch.cuda.synchronize()
+        if clock is not None:
+            clock.mark(1)
+        sync()
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
@@ -259,9 +323,13 @@ def run(args):
 
     for _ in range(args.warmup):
         step()
-    dt = timed(step, args.steps)
+    clock = ClockProbe(dev) if on_gpu else None
+    dt = timed(step, args.steps, clock)
     value = n_global * args.steps / dt
+    clock_ghz, clock_xcd = clock.ghz() if clock is not None else (None, {})
     gf = algorithmic_gflop_per_image(cfg)
+    cls_last = os.environ.get("MICLIP_CLS_LAST", "1").strip() not in ("0", "")   # capi.hip cls_last_block
+    gf_exec = executed_gflop_per_image(cfg, cls_last=cls_last)
 
     ab = None
     if args.ab_splits:
@@ -277,7 +345,7 @@ def run(args):
     if args.ab_fold:
         prev = os.environ.get("MICLIP_LN_FOLD")
         os.environ["MICLIP_LN_FOLD"] = "0"
-        _, m0, _ = miclip.load(args.model, device=dev, compute_dtype=args.dtype)
+        m0 = load_model(args.model, dev, args.dtype)
         if prev is None:
             del os.environ["MICLIP_LN_FOLD"]
         else:
@@ -293,7 +361,8 @@ def run(args):
         abf["fold_median"] = statistics.median(abf["fold"])
         abf["nofold_median"] = statistics.median(abf["nofold"])
         del m0, step0
-        torch.cuda.empty_cache()
+        if on_gpu:
+            torch.cuda.empty_cache()
 
     roofline, kernels = None, None
     prof = None
@@ -302,7 +371,7 @@ def run(args):
         # runs each rank's batch unsplit on one stream, so a GEMM launch has M = b*N
         model.set_profiling(True)
         step()
-        torch.cuda.synchronize()
+        sync()
         prof = model.profile_read(reset=True)
         model.set_profiling(False)
     if rank == 0 and prof is not None:
@@ -328,6 +397,16 @@ def run(args):
                         "algorithmic_flops_per_launch": flops_launch,
                         "avg_launch_ms": round(per_launch_s * 1e3, 4),
                         "traffic_source": tsrc}
+    if roofline is not None:
+        # the clock held over the timed steps (not the profiled one): the peak
+        # scales with it (2.4 GHz nameplate), so frac_at_clock separates the
+        # kernel's schedule from the chip's DVFS state on this box
+        roofline["clock_ghz"] = clock_ghz
+        roofline["clock_ghz_per_xcd"] = clock_xcd
+        roofline["clock_source"] = ("miclip_clock_probe: s_memtime / s_memrealtime per XCD, "
+                                    "before and after the timed steps on the bench stream")
+        roofline["frac_at_clock"] = (round(roofline["frac"] * 2.4 / clock_ghz, 4)
+                                     if clock_ghz else None)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -352,6 +431,11 @@ def run(args):
                        "weights": "seeded random init, CLIP shapes"},
             "gflop_per_image": round(gf, 3),
             "path_mfma_frac": round(value * gf * 1e9 / (world * peak * 1e12), 4),
+            # FLOPs the kernels execute (the last vision block runs on the CLS rows
+            # only, clip/model.py:226-229): the algorithmic figure counts them all
+            "gflop_per_image_executed": round(gf_exec, 3),
+            "path_mfma_frac_executed": round(value * gf_exec * 1e9 / (world * peak * 1e12), 4),
+            "clock_ghz": clock_ghz,
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
         }
         if ab:
@@ -361,6 +445,7 @@ def run(args):
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return line if rank == 0 else None
 
 
 def main():

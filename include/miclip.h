@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MICLIP_ABI_VERSION 5
+#define MICLIP_ABI_VERSION 6
 
 enum miclip_status {
   MICLIP_OK = 0,
@@ -40,7 +40,8 @@ enum miclip_status {
 /* MICLIP_MXFP8: QKV, c_fc and c_proj on OCP MX-fp8 operands (e4m3 + an E8M0 scale
  * per 32 k; weights quantised at load, activations by the producing kernels), the
  * rest as MICLIP_FP16. SURVEY §8f row 4 (C5 fp8 weights); parity unpinned. */
-enum miclip_dtype { MICLIP_FP16 = 0, MICLIP_BF16 = 1, MICLIP_MXFP8 = 2 };
+/* MICLIP_F32: an input element type only (miclip_encode_image_ex images). */
+enum miclip_dtype { MICLIP_FP16 = 0, MICLIP_BF16 = 1, MICLIP_MXFP8 = 2, MICLIP_F32 = 3 };
 enum miclip_act { MICLIP_ACT_QUICKGELU = 1, MICLIP_ACT_GELU = 2 };
 
 /* encode_image flags */
@@ -101,6 +102,14 @@ int miclip_reserve(miclip_model* m, int32_t max_images, int32_t max_prompts);
  * [B, embed_dim] with MICLIP_FLAG_APPLY_PROJ; MICLIP_FLAG_NORMALIZE L2-normalises. */
 int miclip_encode_image(miclip_model* m, const float* images, int32_t B, float* out,
                         uint32_t flags, void* stream);
+
+/* miclip_encode_image with the input batch's element type named:
+ * image_dtype MICLIP_F32, MICLIP_FP16 or MICLIP_BF16 (a device-resident half
+ * batch, e.g. the reference's `images.to(device).half()` under clip.load on GPU,
+ * clip/model.py:336 `image.type(self.dtype)`, read directly by the patchify:
+ * half the input bytes of fp32). Same outputs and flags. */
+int miclip_encode_image_ex(miclip_model* m, const void* images, int32_t image_dtype, int32_t B,
+                           float* out, uint32_t flags, void* stream);
 
 /* Replaces CLIP.encode_text (clip/model.py:338-353), which returns the tuple
  * (x_before_proj [P, transformer_width], x [P, embed_dim]). tokens: device
@@ -179,6 +188,13 @@ int miclip_set_splits(miclip_model* m, int32_t splits);
 /* Parts encode_image splits a batch of B images into (>= 1): at most the
  * miclip_set_splits value, no part below 16 images or 16384 token rows. */
 int miclip_image_splits(const miclip_model* m, int32_t B);
+
+/* Diagnostics (no reference counterpart; SURVEY §8d measurement): n_wg one-wave
+ * workgroups each write {XCD id (HW_REG_XCC_ID), s_memtime (shader-clock
+ * counter), s_memrealtime (100 MHz), 0} as 4 uint64 to device out[4*i..].
+ * Launched before and after a timed region on its stream, the per-XCD ratio of
+ * the two counters' deltas is the core clock the chip held over that region. */
+int miclip_clock_probe(uint64_t* out, int32_t n_wg, void* stream);
 
 void miclip_model_destroy(miclip_model* m);
 const char* miclip_last_error(void);

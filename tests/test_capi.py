@@ -52,7 +52,7 @@ def test_nm_shows_c_linkage():
 
 def test_abi_version_and_validation(lib):
     from miclip import _lib
-    assert lib.miclip_abi_version() == _lib.ABI_VERSION == 5
+    assert lib.miclip_abi_version() == _lib.ABI_VERSION == 6
     bad = _lib.MiclipConfig(embed_dim=512, image_resolution=224, vision_layers=12, vision_width=700,
                             vision_patch_size=32, context_length=77, vocab_size=49408,
                             transformer_width=512, transformer_heads=8, transformer_layers=12,
@@ -70,6 +70,8 @@ def test_abi_version_and_validation(lib):
     assert b"vision_head_dim" in lib.miclip_last_error()
     assert lib.miclip_model_create(None, 0, ctypes.byref(h)) == -1
     assert lib.miclip_op_gemm(0, None, None, None, None, 1, 128, 64, 0, 0, 0, None) == -1
+    assert lib.miclip_encode_image_ex(None, None, _lib.MICLIP_F32, 1, None, 0, None) == -1
+    assert lib.miclip_clock_probe(None, 8, None) == -1
     lib.miclip_model_destroy(None)           # no-op on NULL
     assert lib.miclip_model_bytes(None) == 0
     assert lib.miclip_model_flags(None) == 0

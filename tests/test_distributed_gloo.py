@@ -92,3 +92,67 @@ def test_sharded_feature_cache_matches_single_process(sizes):
         assert feats.shape == tuple(ref_f.shape)
         assert (feats == ref_f.numpy()).all(), "gathered rows differ from the single-process cache"
         assert (labels == ref_l.numpy()).all()
+
+
+class _LoggedDataset:
+    """(image, label) items; records which indices this process read."""
+
+    def __init__(self, n):
+        g = torch.Generator().manual_seed(1)
+        self.x = torch.randn(n, 3, 4, 4, generator=g)
+        self.read = []
+
+    def __len__(self):
+        return len(self.x)
+
+    def __getitem__(self, i):
+        self.read.append(i)
+        return self.x[i], i + 100
+
+
+def _worker_per_rank(rank, world, port, n, bs, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from miclip.feature_cache import ShardedBatchLoader, compute_image_features_sharded
+    ds = _LoggedDataset(n)
+    loader = ShardedBatchLoader(ds, bs)
+    feats, labels = compute_image_features_sharded(StubCLIP(), loader, normalize=True, per_rank=True)
+    q.put((rank, feats.numpy(), labels.numpy(), sorted(ds.read)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n,bs", [(13, 6), (1, 4), (9, 3), (8, 8)])
+def test_per_rank_loader_matches_single_process(n, bs):
+    """Each rank reads and decodes only its contiguous slice of every global batch
+    (ShardedBatchLoader); gather_shards restores the single-process row order of
+    features and labels (aihab_utils/feature_cache.py:144-162)."""
+    from miclip.feature_cache import compute_image_features, shard_range
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world, port = 2, _free_port()
+    procs = [ctx.Process(target=_worker_per_rank, args=(r, world, port, n, bs, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=120)
+        res[r[0]] = r[1:]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ds = _LoggedDataset(n)
+    batches = [(ds.x[b:b + bs], torch.arange(b, min(n, b + bs)) + 100) for b in range(0, n, bs)]
+    model = StubCLIP()
+    ref_f, ref_l = compute_image_features(
+        SimpleNamespace(parameters=model.parameters,
+                        encode_image=lambda x: model.encode_image(x, normalize=True)), batches)
+    for r in range(world):
+        feats, labels, read = res[r]
+        want = []
+        for b in range(0, n, bs):
+            lo, hi = shard_range(min(bs, n - b), r, world)
+            want += list(range(b + lo, b + hi))
+        assert read == want, "a rank read images outside its own slice"
+        assert (feats == ref_f.numpy()).all() and (labels == ref_l.numpy()).all()

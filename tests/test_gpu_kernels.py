@@ -245,6 +245,35 @@ def test_attention_x8(lib, dt, B, N, H):
                                        _stream()) != 0
 
 
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+@pytest.mark.parametrize("N", [257, 258, 259])
+def test_attention_x8_many_heads_per_workgroup(lib, dt, N):
+    """Variant 8 walks hpw > 1 heads per workgroup at the benched batch (2048
+    heads over 2 x 256 slots). The ragged queries' extra keys must be taken
+    before the closing barrier: after it other waves DMA the next head into the
+    same K/V image. Each head's arithmetic does not depend on hpw, so the whole
+    batch must equal, bit for bit, launches of 16 images (256 heads: hpw = 1),
+    on every one of several repeats (a race would vary run to run)."""
+    code, tdt = DT[dt]
+    B, H = 160, 16                     # 2560 heads: hpw = 5 on 256 CUs
+    g = torch.Generator(device="cuda").manual_seed(N + 31)
+    qkv = (torch.randn(B * N, 3 * H * 64, device="cuda", generator=g) * 1.5).to(tdt)
+    ref = torch.empty(B * N, H * 64, device="cuda", dtype=tdt)
+    per = 16
+    esz = ref.element_size()
+    for b0 in range(0, B, per):
+        _check(lib, lib.miclip_op_attention(code, qkv.data_ptr() + b0 * N * 3 * H * 64 * esz,
+                                            ref.data_ptr() + b0 * N * H * 64 * esz, per, N, H, 64,
+                                            0, 8, _stream()))
+    out = torch.empty_like(ref)
+    for _ in range(4):
+        out.fill_(7.0)
+        _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), out.data_ptr(), B, N, H, 64, 0, 8,
+                                            _stream()))
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), f"{(out != ref).sum().item()} elements differ"
+
+
 def test_attention_spike(lib):
     """A key row that dominates one query forces the online-softmax rescale branch."""
     B, N, H = 1, 257, 1

@@ -1,0 +1,166 @@
+"""The open_clip model surface of ViT-H-14 (C5 / PEFT_openclip path).
+
+The reference's open_clip path calls `model.encode_image(images)` and expects the
+POST-projection features (methods/PEFT_openclip.py:90-92: F.normalize -> 100 *
+feats @ text_weights with text_weights [1024, C]), `model.encode_text(tokens)`
+returning ONE [P, 1024] tensor (:38-47, aihab_utils/model_init.py:83-101), and
+caches the normalised post-projection embeddings (aihab_utils/feature_cache.py:
+124-128). miclip.load("ViT-H-14") / open_clip.create_model_and_transforms give
+that surface. Goldens: tests/golden/vith14.npz from the reference's own CLIP
+modules (oracle/make_golden.py); the post-projection image reference is
+`g["image"] @ visual.proj` in float64 on the same seeded weights. open_clip's
+own code is absent, so this row is pinned to the reference graph, not to
+open_clip.
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+COS_TOL = 1e-3
+# MX-fp8 tolerances (tests/test_gpu_parity.py): parity unpinned, fp8 bound
+MX_TOL_IMAGE, MX_TOL_TEXT = 2e-3, 1e-2
+
+_models = {}
+
+
+def _one_minus_cos(a, b, dim=-1):
+    a = torch.as_tensor(a, dtype=torch.float64).cpu()
+    b = torch.as_tensor(b, dtype=torch.float64).cpu()
+    return (1 - F.cosine_similarity(a, b, dim=dim)).numpy()
+
+
+def _model(dtype):
+    import miclip
+    if dtype not in _models:
+        _models.clear()
+        torch.cuda.empty_cache()
+        _models[dtype] = miclip.load("ViT-H-14", device="cuda", compute_dtype=dtype)[1]
+    return _models[dtype]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _needs_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    yield
+    _models.clear()
+
+
+def _refs(g, m):
+    proj = m.state_dict()["visual.proj"].double().cpu()
+    img = torch.from_numpy(g["image"]).double() @ proj                     # [n, 1024]
+    return img, torch.from_numpy(g["text_proj"]).double()
+
+
+def _images(g):
+    from miclip.weights import synthetic_images
+    return torch.from_numpy(synthetic_images(g["meta"]["n_images"], 224, seed=g["meta"]["seed"]))
+
+
+@pytest.mark.parametrize("dtype", ["fp16", "mxfp8"])
+def test_openclip_surface_encoders(golden, dtype):
+    g = golden("vith14")
+    m = _model(dtype)
+    assert m.surface == "open_clip" and m.image_dim == 1024
+    tol_i, tol_t = (COS_TOL, COS_TOL) if dtype == "fp16" else (MX_TOL_IMAGE, MX_TOL_TEXT)
+    ref_img, ref_txt = _refs(g, m)
+    imgs = _images(g).cuda()
+    f = m.encode_image(imgs)
+    assert f.shape == (len(imgs), 1024) and f.dtype == torch.float32
+    d = _one_minus_cos(f, ref_img)
+    fn = m.encode_image(imgs, normalize=True)
+    assert torch.allclose(fn.norm(dim=1), torch.ones(len(imgs), device="cuda"), atol=1e-5)
+    assert torch.allclose(fn, F.normalize(f, dim=-1), atol=1e-5)
+    t = m.encode_text(torch.from_numpy(g["tokens"]).long().cuda())
+    assert isinstance(t, torch.Tensor) and t.shape == (10, 1024)
+    dt = _one_minus_cos(t, ref_txt)
+    tn = m.encode_text(torch.from_numpy(g["tokens"]).long().cuda(), normalize=True)
+    assert torch.allclose(tn, F.normalize(t, dim=-1), atol=1e-6)
+    print(f"ViT-H-14 open_clip surface {dtype}: image 1-cos {d.max():.2e}, text {dt.max():.2e}")
+    assert d.max() <= tol_i and dt.max() <= tol_t
+    # the pre-projection features stay reachable (apply_proj=False)
+    pre = m.encode_image(imgs, apply_proj=False)
+    assert pre.shape == (len(imgs), 1280)
+    # open_clip's forward: (image_features, text_features, logit_scale.exp())
+    fi, ft, scale = m(imgs, torch.from_numpy(g["tokens"]).long().cuda())
+    assert torch.allclose(fi, fn, atol=1e-6) and torch.allclose(ft, tn, atol=1e-6)
+    assert abs(float(scale) - float(m.logit_scale.exp())) < 1e-6
+
+
+@pytest.mark.parametrize("dtype", ["fp16", "mxfp8"])
+def test_openclip_text_weights_and_head(golden, dtype):
+    """_compute_text_weights_from_tokens (methods/PEFT_openclip.py:17-47) and the
+    eval head of _run_validation (:90-95) on the HIP model."""
+    from miclip.classifier import compute_text_weights_from_tokens
+    g = golden("vith14")
+    m = _model(dtype)
+    tol = COS_TOL if dtype == "fp16" else MX_TOL_TEXT
+    toks = torch.from_numpy(g["tokens"]).long()
+    tw = compute_text_weights_from_tokens(m, toks, num_classes=10, num_templates=1)
+    assert tw.shape == (1024, 10)
+    assert _one_minus_cos(tw, g["text_weights"], dim=0).max() <= tol
+    with pytest.raises(ValueError, match="Prompt token count mismatch"):
+        compute_text_weights_from_tokens(m, toks, num_classes=3, num_templates=4)
+    # two templates per class: mean of the normalised prompt embeddings, renormalised
+    tw2 = compute_text_weights_from_tokens(m, toks, num_classes=5, num_templates=2)
+    ref = F.normalize(F.normalize(torch.from_numpy(g["text_proj"]).double(), dim=-1)
+                      .view(5, 2, 1024).mean(1), dim=-1).t()
+    assert _one_minus_cos(tw2, ref, dim=0).max() <= tol
+    # PEFT_openclip eval head: normalize(encode_image) -> 100 * f @ text_weights
+    imgs = _images(g).cuda()
+    feats = F.normalize(m.encode_image(imgs), dim=-1)
+    tw_g = torch.from_numpy(g["text_weights"]).cuda()
+    logits = 100.0 * feats @ tw_g
+    err = (logits.cpu().numpy() - g["logits"]).__abs__().max()
+    sure = g["margins"] > 2 * err
+    assert err < 1.0
+    assert np.array_equal(logits.argmax(1).cpu().numpy()[sure], g["topk"][sure, 0])
+    # the same through the HIP head kernel (features already projected)
+    l2, top = m.zero_shot(m.encode_image(imgs), tw_g, 100.0, k=1, apply_proj=False)
+    assert (l2 - logits).abs().max().item() < 2e-3
+    assert np.array_equal(top[:, 0].cpu().numpy()[sure], g["topk"][sure, 0])
+
+
+def test_openclip_cache_embeddings(golden, tmp_path):
+    """cache_openclip_embeddings on the open_clip surface writes [n, 1024]
+    normalised post-projection embeddings (aihab_utils/feature_cache.py:124-128)."""
+    from miclip.feature_cache import cache_openclip_embeddings
+    g = golden("vith14")
+    m = _model("fp16")
+    imgs = _images(g)
+    n = len(imgs)
+    labels = torch.arange(n)
+    cfg = {"root_path": str(tmp_path), "dataset": "cs", "seed": 1, "clip_backend": "openclip",
+           "open_clip_model": "ViT-H-14",
+           "finetune": {"cache_embeddings_dir": "feat_cache_vis", "cache_embeddings_normalize": True}}
+    d = cache_openclip_embeddings(cfg, m, [(imgs[:1], labels[:1]), (imgs[1:], labels[1:])],
+                                  split="test")
+    assert d == tmp_path / "feat_cache_vis" / "ViT-H-14_cs" / "test" / "seed1"
+    emb = torch.load(d / "embeddings.pt", weights_only=True)
+    assert emb.shape == (n, 1024) and emb.dtype == torch.float32
+    assert torch.allclose(emb.norm(dim=1), torch.ones(n), atol=1e-5)
+    ref_img, _ = _refs(g, m)
+    assert _one_minus_cos(emb, ref_img).max() <= COS_TOL
+    assert json.loads((d / "meta.json").read_text())["dim"] == 1024
+    assert torch.equal(torch.load(d / "labels.pt", weights_only=True), labels)
+
+
+def test_open_clip_module_alias(golden):
+    """`import open_clip` (aihab-clip_amd/open_clip) -> the same model surface."""
+    import open_clip
+    assert "ViT-H-14" in open_clip.list_models()
+    g = golden("vith14")
+    m, pre_train, pre_val = open_clip.create_model_and_transforms("ViT-H-14", pretrained=None,
+                                                                  device="cuda")
+    assert m.surface == "open_clip" and pre_val.n_px == 224
+    ref = _model("fp16")
+    imgs = _images(g).cuda()
+    assert torch.equal(m.encode_image(imgs), ref.encode_image(imgs))
+    with pytest.raises(RuntimeError, match="not found"):
+        open_clip.create_model("ViT-Q-99")
+    del m

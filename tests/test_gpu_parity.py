@@ -38,7 +38,10 @@ def _model(name, dtype):
     if key not in _models:
         _models.clear()
         torch.cuda.empty_cache()
-        _, m, _ = miclip.load(name, device="cuda", compute_dtype=dtype)
+        # the vendored OpenAI surface (pre-projection image features, tuple
+        # encode_text) for every name, ViT-H-14 included: the goldens hold the
+        # pre-projection features (open_clip surface: test_gpu_openclip.py)
+        _, m, _ = miclip.load(name, device="cuda", compute_dtype=dtype, surface="openai")
         _models[key] = m
     return _models[key]
 
