@@ -66,55 +66,63 @@ def resolve_cache_paths(cache_dir: Path) -> CachePaths:
 
 
 def _load_tensor_cpu(path: Path) -> torch.Tensor:
-    loaded = torch.load(path, map_location="cpu", weights_only=True)
-    if not isinstance(loaded, torch.Tensor):
-        raise TypeError(f"Expected tensor at '{path}', got {type(loaded).__name__}.")
-    return loaded
+    """A cache file holds one tensor (loaded with weights_only=True)."""
+    obj = torch.load(path, map_location="cpu", weights_only=True)
+    if isinstance(obj, torch.Tensor):
+        return obj
+    raise TypeError(f"Expected tensor at '{path}', got {type(obj).__name__}.")
 
 
 def _validate_embeddings_labels(embeddings, labels, *, allow_empty=False):
-    if embeddings.ndim != 2:
-        raise ValueError(f"Expected embeddings shape [N, D], got {tuple(embeddings.shape)}.")
-    if labels.ndim == 2 and labels.shape[1] == 1:
-        labels = labels.squeeze(1)
-    if labels.ndim != 1:
-        raise ValueError(f"Expected labels shape [N], got {tuple(labels.shape)}.")
-    if not torch.is_floating_point(embeddings):
-        raise TypeError(f"Expected floating embeddings, got dtype={embeddings.dtype}.")
-    labels = labels.to(torch.long)
-    num_samples, dim = int(embeddings.shape[0]), int(embeddings.shape[1])
-    if int(labels.shape[0]) != num_samples:
-        raise ValueError("Row mismatch between embeddings and labels: "
-                         f"{num_samples} vs {int(labels.shape[0])}.")
-    if not allow_empty and num_samples == 0:
+    """Shape / dtype / row-count checks on an (embeddings [N, D], labels [N]) pair.
+
+    Returns (embeddings, labels as int64 [N], N, D). The error types and texts
+    are the reference's (tools/outlier_cleaning.py), since callers match on them.
+    A [N, 1] label column is accepted as [N]."""
+    if labels.ndim == 2 and labels.shape[-1] == 1:
+        labels = labels[:, 0]
+    checks = (
+        (embeddings.ndim == 2, ValueError,
+         lambda: f"Expected embeddings shape [N, D], got {tuple(embeddings.shape)}."),
+        (labels.ndim == 1, ValueError,
+         lambda: f"Expected labels shape [N], got {tuple(labels.shape)}."),
+        (embeddings.is_floating_point(), TypeError,
+         lambda: f"Expected floating embeddings, got dtype={embeddings.dtype}."),
+    )
+    for ok, exc, msg in checks:
+        if not ok:
+            raise exc(msg())
+    n, d = (int(v) for v in embeddings.shape)
+    if labels.shape[0] != n:
+        raise ValueError(f"Row mismatch between embeddings and labels: {n} vs {int(labels.shape[0])}.")
+    if n == 0 and not allow_empty:
         raise ValueError("Empty inputs: no samples available.")
-    return embeddings, labels, num_samples, dim
+    return embeddings, labels.long(), n, d
 
 
 def load_cache(paths: CachePaths) -> Tuple[torch.Tensor, torch.Tensor, pd.DataFrame]:
-    """Embeddings, labels and metadata with the reference's row-alignment checks."""
-    missing = [p for p in (paths.embeddings, paths.labels, paths.metadata)
-               if not Path(p).is_file()]
-    if missing:
-        raise FileNotFoundError("Missing cache file(s): " + ", ".join(str(p) for p in missing))
-    embeddings = _load_tensor_cpu(paths.embeddings)
-    labels = _load_tensor_cpu(paths.labels)
+    """(embeddings, labels, metadata) of a cache directory, rows cross-checked:
+    the three files exist, embeddings / labels are a consistent pair, metadata.csv
+    has one row per sample with file_name and ground_truth_num_label, and its labels
+    equal labels.pt row for row (the first disagreeing row is reported)."""
+    files = (paths.embeddings, paths.labels, paths.metadata)
+    absent = [str(f) for f in files if not Path(f).is_file()]
+    if absent:
+        raise FileNotFoundError("Missing cache file(s): " + ", ".join(absent))
+    embeddings, labels, n, _ = _validate_embeddings_labels(_load_tensor_cpu(paths.embeddings),
+                                                           _load_tensor_cpu(paths.labels))
     metadata = pd.read_csv(paths.metadata)
-    embeddings, labels, num_samples, _ = _validate_embeddings_labels(embeddings, labels)
-    if int(len(metadata)) != num_samples:
-        raise ValueError("Row mismatch between embeddings and metadata: "
-                         f"{num_samples} vs {int(len(metadata))}.")
-    required = {"file_name", "ground_truth_num_label"}
-    missing_cols = sorted(required - set(metadata.columns))
-    if missing_cols:
-        raise ValueError(f"metadata.csv is missing required column(s): {', '.join(missing_cols)}")
-    meta_labels = torch.tensor(metadata["ground_truth_num_label"].astype(int).to_numpy(),
-                               dtype=torch.long)
-    bad = torch.nonzero(meta_labels != labels, as_tuple=False).flatten()
-    if int(bad.numel()) > 0:
-        i = int(bad[0].item())
+    if len(metadata) != n:
+        raise ValueError(f"Row mismatch between embeddings and metadata: {n} vs {len(metadata)}.")
+    need = sorted({"file_name", "ground_truth_num_label"}.difference(metadata.columns))
+    if need:
+        raise ValueError(f"metadata.csv is missing required column(s): {', '.join(need)}")
+    csv_labels = metadata["ground_truth_num_label"].astype(int).to_numpy()
+    diff = np.flatnonzero(csv_labels != labels.numpy())
+    if diff.size:
+        i = int(diff[0])
         raise ValueError(f"Label mismatch between labels.pt and metadata.csv at row {i}: "
-                         f"labels.pt={int(labels[i])}, metadata.csv={int(meta_labels[i])}.")
+                         f"labels.pt={int(labels[i])}, metadata.csv={int(csv_labels[i])}.")
     return embeddings, labels, metadata
 
 
@@ -217,18 +225,20 @@ class SingleCentroidScorer:
         return uniq, inv.numpy().astype(np.int64)
 
     def _get_normalized_embeddings(self) -> torch.Tensor:
-        if self._normalized_embeddings is not None:
-            return self._normalized_embeddings
-        norms, _ = _row_norms(self.embeddings)
-        if not bool(torch.isfinite(norms).all()):
-            raise ValueError("Non-finite embedding norms found (NaN/Inf).")
-        emb = self.embeddings
-        max_dev = float((norms - 1.0).abs().max().item())
-        if max_dev > self.normalize_tol:
-            print(f"[warn] Unnormalized embeddings detected (max |norm-1|={max_dev:.3e}); normalizing.")
-            _, emb = _row_norms(self.embeddings, self.eps, normalize=True)
-        self._normalized_embeddings = emb
-        return emb
+        """Unit-norm rows on the device, computed once: the row norms come from the
+        HIP kernel; rows are re-normalised (same kernel) only when some norm is off
+        by more than normalize_tol; NaN / Inf norms are an error."""
+        if self._normalized_embeddings is None:
+            norms, _ = _row_norms(self.embeddings)
+            if not torch.isfinite(norms).all().item():
+                raise ValueError("Non-finite embedding norms found (NaN/Inf).")
+            worst = (norms - 1.0).abs().max().item()
+            emb = self.embeddings
+            if worst > self.normalize_tol:
+                print(f"[warn] Unnormalized embeddings detected (max |norm-1|={worst:.3e}); normalizing.")
+                emb = _row_norms(self.embeddings, self.eps, normalize=True)[1]
+            self._normalized_embeddings = emb
+        return self._normalized_embeddings
 
     def compute_centroids(self, *, trim_frac: Optional[float] = None) -> CentroidResult:
         if trim_frac is not None:
