@@ -57,7 +57,7 @@ def test_large_batch_config(golden, tag, name, dtype, bs, splits, tol):
     gold = synthetic_images(n, R, seed=g["meta"]["seed"])
     batch = synthetic_images(bs, R, seed=77)
     half = bs // 2
-    rows = sorted({0, half - 1, half, bs - 1} | {1 + 37 * i for i in range(n)})
+    rows = sorted({0, half - 1, half, bs - 1} | {3 + (bs // n) * i for i in range(n)})
     src = [i % n for i in range(len(rows))]
     batch[rows] = gold[src]
     _, m, _ = miclip.load(name, device="cuda", compute_dtype=dtype, surface="openai")
