@@ -1758,6 +1758,345 @@ __global__ __launch_bounds__(256, 2) void gemm_t2_kernel(const T* __restrict__ A
   }
 }
 
+// ---------------------------------------------------------------------------
+// Ping-pong persistent GEMM (variant 400): TWO workgroups per CU, each 4 waves
+// (one per SIMD) walking 256x128 tiles with its own LDS ring, so one
+// workgroup's epilogue (VALU-bound: folded LN, QuickGELU, conversion; or the
+// residual read-modify-write) runs beside the other workgroup's MFMA main loop
+// on every SIMD instead of idling the matrix pipes (the 8-wave 256x256 kernel
+// spends ~23 % of a c_fc launch in its epilogue with the pipes idle).
+//   * per wave 128x64 outputs (8x4 16x16 fp32 fragments, 128 registers), the
+//     MFMA operands swapped for TrAcc epilogues (lane = row fr, 4 consecutive
+//     columns) exactly as the 8-wave kernel, same v_mfma_f32_16x16x32 chain in
+//     the same k order (32-k steps ascending), so tiles, tails and the other
+//     kernels stay bit-identical (batch invariance);
+//   * K in 32-k steps through a 3-slot ring (A 256 x 64 B + W 128 x 64 B =
+//     24 KiB per slot), LDS-DMA 2 steps ahead; fragments for step g+1 are read
+//     (into the other register set) before step g's MFMAs, so the only waits are
+//     one counted vmcnt + one 4-wave barrier per step. The ring runs on across
+//     tiles: the next tile's first steps are in flight (and its first
+//     fragments in registers) while this tile's epilogue runs;
+//   * 64-B LDS rows, 16-B chunk c of row r at c ^ ((r >> 1) & 3): conflict-free
+//     ds_read_b128 fragment reads under gfx950's lane groups;
+//   * register epilogue: one v_permlane16_swap per dword turns two row blocks'
+//     8-B column quads into 16-B row pieces (8 columns of one row per lane),
+//     stored straight from registers: no LDS staging, so the ring never stops;
+//   * the second workgroup on each CU starts `delay` 100-MHz ticks late so the
+//     two run half an epilogue out of phase (in phase, their epilogues would
+//     coincide and nothing would overlap).
+// The last tile-row may be partial (rows clamped on load, guarded on store).
+// ---------------------------------------------------------------------------
+// 16-byte LDS-DMA through a buffer descriptor (buffer_load_dwordx4 ... lds): byte
+// offset = lane part `vlane` (a VGPR) + wave-uniform part `soff` (an SGPR), added
+// INSIDE the statement so hipcc cannot strength-reduce the offsets into one
+// live VGPR per DMA (its loop-carried copies spilled, and the reloads put
+// vmcnt(0) waits into the K loop); `lds` an LDS byte address (wave-uniform).
+// The whole offset is range-checked: lanes past the descriptor's byte count
+// fetch nothing (rows past M of a partial tile: never stored).
+MICLIP_DEV void bdma16(unsigned vlane, unsigned soff, __amdgpu_buffer_rsrc_t rsrc, unsigned lds) {
+  unsigned keep, tmp;
+  asm volatile(
+      "v_add_u32 %1, %3, %2\n\t"
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %5\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %4, 0 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep), "=&v"(tmp)
+      : "v"(vlane), "s"(soff), "s"(rsrc), "s"(lds)
+      : "memory");
+}
+
+// s_waitcnt vmcnt(n), n wave-uniform in [0, 63]
+MICLIP_DEV void wait_vmcnt63(int n) {
+  switch (n) {
+#define MICLIP_VMC(k) \
+  case k:           \
+    asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    MICLIP_VMC(0) MICLIP_VMC(1) MICLIP_VMC(2) MICLIP_VMC(3) MICLIP_VMC(4) MICLIP_VMC(5)
+    MICLIP_VMC(6) MICLIP_VMC(7) MICLIP_VMC(8) MICLIP_VMC(9) MICLIP_VMC(10) MICLIP_VMC(11)
+    MICLIP_VMC(12) MICLIP_VMC(13) MICLIP_VMC(14) MICLIP_VMC(15) MICLIP_VMC(16) MICLIP_VMC(17)
+    MICLIP_VMC(18) MICLIP_VMC(19) MICLIP_VMC(20) MICLIP_VMC(21) MICLIP_VMC(22) MICLIP_VMC(23)
+    MICLIP_VMC(24) MICLIP_VMC(25) MICLIP_VMC(26) MICLIP_VMC(27) MICLIP_VMC(28) MICLIP_VMC(29)
+    MICLIP_VMC(30) MICLIP_VMC(31) MICLIP_VMC(32) MICLIP_VMC(33) MICLIP_VMC(34) MICLIP_VMC(35)
+    MICLIP_VMC(36) MICLIP_VMC(37) MICLIP_VMC(38) MICLIP_VMC(39) MICLIP_VMC(40) MICLIP_VMC(41)
+    MICLIP_VMC(42) MICLIP_VMC(43) MICLIP_VMC(44) MICLIP_VMC(45) MICLIP_VMC(46) MICLIP_VMC(47)
+#undef MICLIP_VMC
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// epilogue global operations per lane of a full tile (stores, + residual loads)
+template <class Epi> struct PPEpiOps { static constexpr int n = 16; };
+template <> struct PPEpiOps<EpiResidual<_Float16>> { static constexpr int n = 32; };
+
+// 4-byte LDS-DMA of one dword into a dead LDS word: pads a wave's VM counter so
+// every wave's counted waits use the same compile-time counts
+MICLIP_DEV void vm_pad(const void* g, const void* lds) { glds4_hidden(g, lds); }
+
+template <typename T, class Epi>
+__global__ __launch_bounds__(256, 2) void gemm_pp_kernel(const T* __restrict__ A,
+                                                         const T* __restrict__ W, int M, int N,
+                                                         int K, Epi epi, int gm, int ntm,
+                                                         int delay) {
+  static_assert(TrAcc<Epi>::value, "gemm_pp_kernel: transposed-accumulator epilogues only");
+  constexpr int NS = 3, A_BYTES = 256 * 64, STAGE = A_BYTES + 128 * 64;   // 16 + 8 KiB
+  constexpr int OPS = NS * STAGE;
+  constexpr bool LN = IsLN<Epi>::value;
+  constexpr bool RES = PrefetchX<Epi>::value;
+  // VM-counter bookkeeping (per lane, per wave): D = LDS-DMA per step, C = the
+  // operand DMAs at a tile's first step (bias / column sums by wave 0, the row
+  // statistics by every wave, padded to the same count on every wave), E = the
+  // epilogue's global ops (stores, + residual loads)
+  constexpr int D = 6, C = LN ? 3 : 1, E = PPEpiOps<Epi>::n;
+  __shared__ __attribute__((aligned(1024))) char smem[OPS + 4096];
+  float4* tbias = (float4*)(smem + OPS);            // [32] bias column quads
+  float4* tcs = (float4*)(smem + OPS + 512);        // [32] column-sum quads (LN)
+  float2* tst = (float2*)(smem + OPS + 1024);       // [256] {mean, rstd} (LN)
+  char* sink = smem + OPS + 3072;                   // vm_pad destination (never read)
+
+  const int ntn = N / 128, ntiles = ntm * ntn, nk = K / 32;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int swz = (fk ^ ((fr >> 1) & 3)) << 4;
+  const int aoff = (wr * 128 + fr) * 64 + swz;
+  const int boff = A_BYTES + (wc * 64 + fr) * 64 + swz;
+  const int prow = lane >> 2, lch = (lane & 3) ^ ((lane >> 3) & 3);
+
+  if (delay > 0 && (int)blockIdx.x >= (int)(gridDim.x >> 1)) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)delay)
+      __builtin_amdgcn_s_sleep(8);
+  }
+
+  // LDS-DMA through buffer descriptors: per lane one VGPR (its row and 16-B
+  // chunk within a 16-row piece), the rest wave-uniform; A rows past M fall
+  // outside A's descriptor (partial last tile-row)
+  const unsigned lbase = (unsigned)prow * (unsigned)K * 2u + (unsigned)lch * 16u;
+  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)A, (short)0, (int)((unsigned)M * (unsigned)K * 2u), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)W, (short)0, (int)((unsigned)N * (unsigned)K * 2u), 0x00020000);
+  const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(LDS_AS char*)smem);
+  unsigned arow0 = 0, brow0 = 0;   // byte offsets of the fetched tile's first A / W row
+  auto set_sources = [&](int m0_, int n0_) {
+    arow0 = (unsigned)(m0_ + wave * 64) * (unsigned)K * 2u;
+    brow0 = (unsigned)(n0_ + wave * 32) * (unsigned)K * 2u;
+  };
+  const unsigned piece_bytes = 16u * (unsigned)K * 2u;
+  auto dma_step = [&](int t, int slot_) {
+    const unsigned st = lds0 + slot_ * STAGE;
+    const unsigned kb = (unsigned)t * 64u;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      bdma16(lbase, __builtin_amdgcn_readfirstlane(arow0 + p * piece_bytes + kb), arsrc,
+             st + (wave * 4 + p) * 1024);
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      bdma16(lbase, __builtin_amdgcn_readfirstlane(brow0 + p * piece_bytes + kb), wrsrc,
+             st + A_BYTES + (wave * 2 + p) * 1024);
+  };
+  auto tile_of = [&](int id, int& m0_, int& n0_) {
+    int tm, tn;
+    group_tile(xcd_remap(id, ntiles), ntm, ntn, gm, tm, tn);
+    m0_ = tm * 256;
+    n0_ = tn * 128;
+  };
+  // the tile's epilogue operands into LDS (retired by the step waits, published by
+  // the step barriers long before the epilogue reads them): exactly C per wave
+  auto dma_operands = [&](int m0_, int n0_) {
+    int lo = lane;
+    asm volatile("" : "+v"(lo));
+    if (wave == 0) {
+      const float* src = epi.bias + n0_ + (lo & 31) * 4;
+      if constexpr (LN) {
+        if (lo >= 32) src = epi.colsum + n0_ + (lo & 31) * 4;
+      }
+      glds16_hidden(src, tbias);
+    } else {
+      vm_pad(epi.bias, sink);
+    }
+    if constexpr (LN) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int d = wave * 128 + h * 64 + lo, r = m0_ + (d >> 1);
+        glds4_hidden((const float*)(epi.stats + (r < M ? r : M - 1)) + (d & 1),
+                     (const char*)tst + wave * 512 + h * 256);
+      }
+    }
+  };
+
+  f32x4 acc[8][4];
+  // A fragments single-buffered (fa[i] is reloaded for the next step right after
+  // its last MFMA of this step), W fragments double-buffered (every A fragment
+  // meets all four): 64 fragment VGPRs beside the 128 accumulators
+  i16x8 fa[8], fb[2][4];
+  auto read_a = [&](int slot_, int i) {
+    fa[i] = *(const i16x8*)(smem + slot_ * STAGE + aoff + i * 1024);
+  };
+  auto read_b = [&](int slot_, auto par_c) {
+    constexpr int P = decltype(par_c)::value;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[P][j] = *(const i16x8*)(smem + slot_ * STAGE + boff + j * 1024);
+  };
+  // step's MFMAs (W fragments of set P); nslot >= 0: read the next step's A
+  // fragments from that slot as this step's uses of them end
+  auto mfmas = [&](auto par_c, auto first_c, int nslot) {
+    constexpr int P = decltype(par_c)::value;
+    constexpr bool FIRST = decltype(first_c)::value;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 c = FIRST ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j];
+        acc[i][j] = Mfma<T>::m16(fb[P][j], fa[i], c);   // C^T = W . A^T
+      }
+      if (nslot >= 0) read_a(nslot, i);
+    }
+  };
+
+  int id = blockIdx.x;
+  if (id >= ntiles) return;
+  int m0, n0;
+  tile_of(id, m0, n0);
+  set_sources(m0, n0);
+  // prologue: steps 0..2 in flight, E pad DMAs standing in for a previous tile's
+  // epilogue ops (so the first tile's counted waits are the steady-state ones),
+  // step 0 landed and its fragments read
+  int slot = 0;                  // slot of the current step
+  dma_step(0, 0);
+  dma_step(1, 1);
+  dma_step(2, 2);
+#pragma unroll
+  for (int e = 0; e < E; ++e) vm_pad(epi.bias, sink);
+  wait_vmcnt63(2 * D + E);
+  lds_barrier();
+  read_b(0, std::integral_constant<int, 0>{});
+#pragma unroll
+  for (int i = 0; i < 8; ++i) read_a(0, i);
+  __builtin_amdgcn_s_setprio(1);
+  for (;;) {
+    const int nid = id + gridDim.x;
+    const bool has_next = nid < ntiles;
+    int nm0 = 0, nn0 = 0;
+    if (has_next) tile_of(nid, nm0, nn0);
+    const bool full = m0 + 256 <= M;
+    // one 32-k step: t = local step, P = register set holding step t's fragments.
+    // Ops issued after step t+1's DMA (at step t-2) in the steady stream: the DMA
+    // of step t+2, and for t <= 2 the epilogue ops between the tiles (t = 0, 1)
+    // and the operand DMAs of this tile's first step (t = 1, 2). One body for
+    // every t (a peeled copy per t made hipcc rename, copy and spill
+    // accumulators), the count picked by a wave-uniform branch.
+    auto step = [&](int t, auto par_c) {
+      constexpr int P = decltype(par_c)::value;
+      const bool tail = !has_next && t + 2 >= nk;   // the stream's last two steps
+      if (!tail) {
+        switch (t < 3 ? t : 3) {
+          case 0: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D + E) : "memory"); break;
+          case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D + E + C) : "memory"); break;
+          case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D + C) : "memory"); break;
+          default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D) : "memory"); break;
+        }
+      } else if (t + 2 == nk) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no step t+2 exists
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      lds_barrier();
+      // refill the slot step t's fragments were read from (every wave is past
+      // this barrier, its reads retired by the lgkmcnt above)
+      if (t + 3 < nk) {
+        dma_step(t + 3, slot);
+      } else if (has_next) {
+        if (t + 3 == nk) set_sources(nm0, nn0);
+        dma_step(t + 3 - nk, slot);
+      }
+      if (t == 0) dma_operands(m0, n0);
+      const int nslot = slot == NS - 1 ? 0 : slot + 1;
+      // the next tile's first fragments are read after the epilogue (not live
+      // across it: the epilogue needs the registers)
+      const bool more1 = t + 1 < nk;
+      if (more1) read_b(nslot, std::integral_constant<int, P ^ 1>{});
+      mfmas(par_c, std::false_type{}, more1 ? nslot : -1);
+      slot = nslot;
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < nk; t += 2) {
+      step(t, I0{});
+      step(t + 1, I1{});
+    }
+
+    // ---- epilogue from registers (TR: lane = row fr, columns 4fk .. 4fk+3) ----
+    __builtin_amdgcn_s_setprio(0);
+    auto* cb = tr_out(epi);
+    const int ld = tr_ld(epi);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      // rows of blocks 2p (lanes fk even) and 2p+1 (fk odd) after the swap
+      const int row = m0 + wr * 128 + (2 * p + (fk & 1)) * 16 + fr;
+      const int rowc = row < M ? row : M - 1;
+      const int col = n0 + wc * 64 + (fk >> 1) * 8;
+      u32x4 xq[4];
+      if constexpr (RES) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xq[j] = *(const u32x4*)(cb + (size_t)rowc * ld + col + j * 16);
+      }
+      float2 s0 = make_float2(0.f, 0.f), s1 = make_float2(0.f, 0.f);
+      if constexpr (LN) {
+        s0 = tst[wr * 128 + (2 * p) * 16 + fr];
+        s1 = tst[wr * 128 + (2 * p + 1) * 16 + fr];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 bq = tbias[wc * 16 + j * 4 + fk];
+        const f32x4 a0 = acc[2 * p][j], a1 = acc[2 * p + 1][j];
+        const float4 v0 = make_float4(a0[0], a0[1], a0[2], a0[3]);
+        const float4 v1 = make_float4(a1[0], a1[1], a1[2], a1[3]);
+        i16x4 o0, o1;
+        if constexpr (LN) {
+          const float4 cq = tcs[wc * 16 + j * 4 + fk];
+          o0 = epi.val4ln(v0, bq, cq, s0);
+          o1 = epi.val4ln(v1, bq, cq, s1);
+        } else {
+          o0 = epi.val4(v0, bq);
+          o1 = epi.val4(v1, bq);
+        }
+        const u32x2 u = __builtin_bit_cast(u32x2, o0), v = __builtin_bit_cast(u32x2, o1);
+        // 16-lane rows: the fk-odd rows of u <-> the fk-even rows of v
+        const auto w0 = __builtin_amdgcn_permlane16_swap(u[0], v[0], false, false);
+        const auto w1 = __builtin_amdgcn_permlane16_swap(u[1], v[1], false, false);
+        u32x4 w = {w0[0], w1[0], w0[1], w1[1]};
+        if constexpr (RES) {
+          unsigned tt[4] = {w[0], w[1], w[2], w[3]};
+          const unsigned xx[4] = {xq[j][0], xq[j][1], xq[j][2], xq[j][3]};
+          Epi::template add_x<4>(tt, xx);
+          w = (u32x4){tt[0], tt[1], tt[2], tt[3]};
+        }
+        if (full || row < M) *(u32x4*)(cb + (size_t)row * ld + col + j * 16) = w;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_setprio(1);
+    if (!has_next) break;
+    // the next tile's step-0 fragments (its DMA was retired and published at
+    // this tile's last step)
+    read_b(slot, std::integral_constant<int, 0>{});
+#pragma unroll
+    for (int i = 0; i < 8; ++i) read_a(slot, i);
+    // a partial tile issued fewer than E ops: drain, so the next tile's counted
+    // waits (which assume E younger ops) can only over-wait
+    if (!full) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    id = nid;
+    m0 = nm0;
+    n0 = nn0;
+  }
+  // nothing may land in LDS after the workgroup retires
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // MICLIP_GEMM=128 forces the 128x128 kernel (A/B comparisons), 256 forces the
 // 256x256 one wherever the shape allows; default picks by problem size.
 int gemm_variant() {
@@ -1881,8 +2220,22 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   variant %= 1000;
   if (variant == 0) variant = gemm_variant();
   if (variant != 0 && variant != 128 && variant != 256 && variant != 257 && variant != 258 &&
-      variant != 259 && variant != 260 && variant != 2 && variant != 3 && variant != 300)
+      variant != 259 && variant != 260 && variant != 2 && variant != 3 && variant != 300 &&
+      !(variant >= 400 && variant < 420))
     return hipErrorInvalidValue;
+  if constexpr (TrAcc<Epi>::value && !std::is_same_v<Epi, EpiResidual<float>>) {
+    // ping-pong kernel: variant 400 + d = start delay of the second workgroup per
+    // CU in microseconds
+    if (variant >= 400 && variant < 420) {
+      if (N % 128 || K % 64 || K < 128 || !epi.bias) return hipErrorInvalidValue;
+      const int ntm = (M + 255) / 256, ntiles = ntm * (N / 128), ncu = cu_count();
+      const int grid = ntiles < 2 * ncu ? ntiles : 2 * ncu;
+      hipLaunchKernelGGL((gemm_pp_kernel<T, Epi>), dim3(grid), dim3(256), 0, s, (const T*)A,
+                         (const T*)W, M, N, K, epi, gm, ntm, (variant - 400) * 100);
+      return hipGetLastError();
+    }
+  }
+  if (variant >= 400 && variant < 420) return hipErrorInvalidValue;
   if constexpr (!IsPatch<Epi>::value) {
     if (variant == 300 && N % 256 == 0 && K % 64 == 0) {
       // 4-wave 128x128-per-wave kernel (A/B prototype), one tile per workgroup
