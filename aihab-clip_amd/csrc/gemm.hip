@@ -913,15 +913,9 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
   };
   // FIRST (K-tile 0): the k-step-0 MFMAs take a zero accumulator operand (the
   // inline constant 0), so a tile needs no 128 v_mov zeroing its accumulators
-  // MFMA issue priority (tail_wide bits 4-5; MICLIP_GEMM_PRIO / kGemmPrio A/B):
-  // 0 = s_setprio 1 around every phase's MFMAs (all waves), 1 = a static
-  // s_setprio 1 for waves 4-7 (the staggered, younger half: MI355X_MICROARCH.md
-  // "Two waves per SIMD" item 4), 2 = none
-  const int prio_mode = (tail_wide >> 4) & 3;
-  if (prio_mode == 1 && wr == 1) __builtin_amdgcn_s_setprio(1);
   auto mfma_q = [&](int qi, int qj, auto first_c) {
     constexpr bool FIRST = decltype(first_c)::value;
-    if (prio_mode == 0) __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -934,7 +928,7 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
           else
             acc[qi][qj][i][j] = Mfma<T>::m16(af[s][i], bf[s][j], c);
         }
-    if (prio_mode == 0) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(0);
   };
 
   int prev_stores = -1;   // -1: first tile (full prologue)
@@ -1310,7 +1304,7 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
   // the row tail on the same workgroups
   for (int task = blockIdx.x; task < ntail; task += gridDim.x) {
     lds_barrier();
-    if (tail_wide & 1)
+    if (tail_wide)
       gemm_tail_wg<T, Epi, 2, 128>(A, W, M, N, K, epi, ntm * 256, task, smem);
     else
       gemm_tail_wg<T, Epi, 1, 64>(A, W, M, N, K, epi, ntm * 256, task, smem);
@@ -2154,16 +2148,6 @@ constexpr int kGemmNoTail = 1 << 16;
 constexpr int kGemmTailFirst = 1 << 17;
 // kGemmStagger (8 us) / MICLIP_GEMM_STAGGER=<us>: round stagger, see gemm256_kernel
 constexpr int kGemmStagger = 1 << 18;
-// variant bits 19-20 (1 + mode): persistent kernel MFMA priority mode, see
-// gemm256s_kernel; MICLIP_GEMM_PRIO=<mode> sets the default (0)
-constexpr int kGemmPrioShift = 19;
-int gemm_prio() {
-  static int p = [] {
-    const char* e = getenv("MICLIP_GEMM_PRIO");
-    return e ? (atoi(e) & 3) : 0;
-  }();
-  return p;
-}
 int gemm_stagger_us() {
   static int us = [] {
     const char* e = getenv("MICLIP_GEMM_STAGGER");
@@ -2231,8 +2215,7 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   const bool notail = (variant & kGemmNoTail) || !gemm_tail_enabled();
   const bool tail_first = variant & kGemmTailFirst;
   const bool stagger = variant & kGemmStagger;
-  const int prio = variant & (3 << kGemmPrioShift) ? ((variant >> kGemmPrioShift) & 3) - 1 : gemm_prio();
-  variant &= ~(kGemmNoTail | kGemmTailFirst | kGemmStagger | (3 << kGemmPrioShift));
+  variant &= ~(kGemmNoTail | kGemmTailFirst | kGemmStagger);
   const int gm = variant >= 1000 ? variant / 1000 : gemm_group();
   variant %= 1000;
   if (variant == 0) variant = gemm_variant();
@@ -2279,13 +2262,12 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
       if (!gemm_tracc()) {
         hipLaunchKernelGGL((gemm256s_kernel<T, Epi, false>), dim3(grid), dim3(512), 0, s,
                            (const T*)A, (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs,
-                           (tp.wide & 1) | (prio << 4));
+                           tp.wide & 1);
         return hipGetLastError();
       }
     }
     hipLaunchKernelGGL((gemm256s_kernel<T, Epi>), dim3(grid), dim3(512), 0, s, (const T*)A,
-                       (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs,
-                       (tp.wide & 1) | (prio << 4));
+                       (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs, tp.wide & 1);
     return hipGetLastError();
   }
   if (variant == 3) {   // persistent 256x256
