@@ -101,7 +101,7 @@ def main():
         qkv = (torch.randn(M, 3 * W, device="cuda", generator=g)).to(dt)
         o = torch.empty(M, W, device="cuda", dtype=dt)
 
-        avs = (2, 4, 8, 2, 4, 8) if 256 <= args.tokens < 288 else (0, 1, 0, 1)
+        avs = (8, 9, 8, 9, 8, 9, 2) if 257 <= args.tokens <= 259 else (0, 1, 0, 1)
         for av in (avs if dh == 64 else (0, 0)):
             def fa():
                 rc = lib.miclip_op_attention(0, qkv.data_ptr(), o.data_ptr(), args.batch, args.tokens, H, dh,

@@ -274,6 +274,45 @@ def test_attention_x8_many_heads_per_workgroup(lib, dt, N):
         assert torch.equal(out, ref), f"{(out != ref).sum().item()} elements differ"
 
 
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+@pytest.mark.parametrize("B,N,H", [(1, 257, 1), (37, 257, 16), (160, 257, 16), (5, 258, 4),
+                                   (2, 259, 2), (24, 259, 16), (3, 258, 7)])
+def test_attention_stream(lib, dt, B, N, H):
+    """Streamed kernel (variant 9): key tiles through an LDS ring across a
+    workgroup's heads (hpw 1..5 here). The 8 full query chunks run the x8
+    kernel's arithmetic in its order, so those rows equal variant 8's bit for
+    bit; the ragged rows 256.. (VALU partials, another summation order) agree
+    to rounding. Repeats must be identical (a ring race would vary)."""
+    code, tdt = DT[dt]
+    g = torch.Generator(device="cuda").manual_seed(B * 1000 + N + H + 9)
+    qkv = (torch.randn(B * N, 3 * H * 64, device="cuda", generator=g) * 1.5).to(tdt)
+    ref8 = torch.empty(B * N, H * 64, device="cuda", dtype=tdt)
+    _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), ref8.data_ptr(), B, N, H, 64, 0, 8,
+                                        _stream()))
+    out = torch.empty_like(ref8)
+    first = None
+    for _ in range(3):
+        out.fill_(7.0)
+        _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), out.data_ptr(), B, N, H, 64, 0, 9,
+                                            _stream()))
+        torch.cuda.synchronize()
+        if first is None:
+            first = out.clone()
+        else:
+            assert torch.equal(out, first), f"{(out != first).sum().item()} elements vary"
+    ref = _attn_ref(qkv, B, N, H, 0)
+    err = (out.float() - ref).abs().max().item()
+    assert err < (4e-2 if dt == "bf16" else 6e-3), err
+    o3, r3 = out.view(B, N, -1), ref8.view(B, N, -1)
+    full = torch.equal(o3[:, :256], r3[:, :256])
+    assert full, f"{(o3[:, :256] != r3[:, :256]).sum().item()} full-chunk elements differ from variant 8"
+    rag = (o3[:, 256:].float() - r3[:, 256:].float()).abs().max().item()
+    assert rag < (1.6e-2 if dt == "bf16" else 2e-3), rag
+    for n, causal in ((256, 0), (260, 0), (200, 0), (257, 1)):
+        assert lib.miclip_op_attention(code, qkv.data_ptr(), out.data_ptr(), 1, n, H, 64, causal, 9,
+                                       _stream()) != 0
+
+
 def test_attention_spike(lib):
     """A key row that dominates one query forces the online-softmax rescale branch."""
     B, N, H = 1, 257, 1
