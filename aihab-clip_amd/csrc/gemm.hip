@@ -2218,6 +2218,7 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   variant &= ~(kGemmNoTail | kGemmTailFirst | kGemmStagger);
   const int gm = variant >= 1000 ? variant / 1000 : gemm_group();
   variant %= 1000;
+  const bool env_variant = variant == 0;   // MICLIP_GEMM: falls back where it does not apply
   if (variant == 0) variant = gemm_variant();
   if (variant != 0 && variant != 128 && variant != 256 && variant != 257 && variant != 258 &&
       variant != 259 && variant != 260 && variant != 2 && variant != 3 && variant != 300 &&
@@ -2227,7 +2228,12 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
     // ping-pong kernel: variant 400 + d = start delay of the second workgroup per
     // CU in microseconds
     if (variant >= 400 && variant < 420) {
-      if (N % 128 || K % 64 || K < 128 || !epi.bias) return hipErrorInvalidValue;
+      if (N % 128 || K % 64 || K < 128 || !epi.bias) {
+        if (!env_variant) return hipErrorInvalidValue;
+        variant = 0;
+      }
+    }
+    if (variant >= 400 && variant < 420) {
       const int ntm = (M + 255) / 256, ntiles = ntm * (N / 128), ncu = cu_count();
       const int grid = ntiles < 2 * ncu ? ntiles : 2 * ncu;
       hipLaunchKernelGGL((gemm_pp_kernel<T, Epi>), dim3(grid), dim3(256), 0, s, (const T*)A,
@@ -2235,7 +2241,10 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
       return hipGetLastError();
     }
   }
-  if (variant >= 400 && variant < 420) return hipErrorInvalidValue;
+  if (variant >= 400 && variant < 420) {
+    if (!env_variant) return hipErrorInvalidValue;
+    variant = 0;
+  }
   if constexpr (!IsPatch<Epi>::value) {
     if (variant == 300 && N % 256 == 0 && K % 64 == 0) {
       // 4-wave 128x128-per-wave kernel (A/B prototype), one tile per workgroup
