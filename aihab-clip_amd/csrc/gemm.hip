@@ -827,7 +827,11 @@ MICLIP_DEV void wait_vmcnt_tile(int n) {
   }
 }
 
-template <typename T, class Epi, bool TRQ = true>
+// DIAG (diagnostic builds of the main loop, outputs meaningless): 1 = the
+// K-tile DMAs of every odd K-tile are skipped (the loop reuses stale LDS), 2 =
+// only K-tiles 0 and 1 are fetched. Used to tell the L2->LDS path from the
+// schedule as the main loop's limit (scripts/bench_ops.py variant suffixes).
+template <typename T, class Epi, bool TRQ = true, int DIAG = 0>
 __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
                                                        const T* __restrict__ W, int M, int N,
                                                        int K, Epi epi, int gm, int ntm_dp,
@@ -884,6 +888,12 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
   const T* asrc[2][2];
   const T* bsrc[2][2];
   auto stage = [&](int slot_kind, int tile) {
+    if constexpr (DIAG == 1) {
+      if (tile & 1) return;
+    }
+    if constexpr (DIAG == 2) {
+      if (tile >= 2) return;
+    }
     const int buf = tile & 1, k0 = tile * 64;
     char* dst = smem + (buf * 4 + slot_kind) * HALF + wave * 2048;
     const T* const* src = slot_kind < 2 ? asrc[slot_kind] : bsrc[slot_kind - 2];
@@ -2148,6 +2158,9 @@ constexpr int kGemmNoTail = 1 << 16;
 constexpr int kGemmTailFirst = 1 << 17;
 // kGemmStagger (8 us) / MICLIP_GEMM_STAGGER=<us>: round stagger, see gemm256_kernel
 constexpr int kGemmStagger = 1 << 18;
+// kGemmDiag1 / kGemmDiag2: gemm256s_kernel DIAG 1 / 2 (diagnostic, garbage output)
+constexpr int kGemmDiag1 = 1 << 19;
+constexpr int kGemmDiag2 = 1 << 20;
 int gemm_stagger_us() {
   static int us = [] {
     const char* e = getenv("MICLIP_GEMM_STAGGER");
@@ -2215,7 +2228,8 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   const bool notail = (variant & kGemmNoTail) || !gemm_tail_enabled();
   const bool tail_first = variant & kGemmTailFirst;
   const bool stagger = variant & kGemmStagger;
-  variant &= ~(kGemmNoTail | kGemmTailFirst | kGemmStagger);
+  const int diag = variant & kGemmDiag1 ? 1 : variant & kGemmDiag2 ? 2 : 0;
+  variant &= ~(kGemmNoTail | kGemmTailFirst | kGemmStagger | kGemmDiag1 | kGemmDiag2);
   const int gm = variant >= 1000 ? variant / 1000 : gemm_group();
   variant %= 1000;
   const bool env_variant = variant == 0;   // MICLIP_GEMM: falls back where it does not apply
@@ -2270,6 +2284,21 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
     if constexpr (TrAcc<Epi>::value) {
       if (!gemm_tracc()) {
         hipLaunchKernelGGL((gemm256s_kernel<T, Epi, false>), dim3(grid), dim3(512), 0, s,
+                           (const T*)A, (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs,
+                           tp.wide & 1);
+        return hipGetLastError();
+      }
+    }
+    if constexpr (std::is_same_v<Epi, EpiResidual<_Float16>> ||
+                  std::is_same_v<Epi, EpiStore<_Float16, ACT_QUICKGELU>>) {
+      if (diag == 1) {
+        hipLaunchKernelGGL((gemm256s_kernel<T, Epi, true, 1>), dim3(grid), dim3(512), 0, s,
+                           (const T*)A, (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs,
+                           tp.wide & 1);
+        return hipGetLastError();
+      }
+      if (diag == 2) {
+        hipLaunchKernelGGL((gemm256s_kernel<T, Epi, true, 2>), dim3(grid), dim3(512), 0, s,
                            (const T*)A, (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs,
                            tp.wide & 1);
         return hipGetLastError();
