@@ -343,6 +343,19 @@ int ensure_folded(miclip_model* m, bool visual) {
 // same operations as the full block (GEMM rows are independent; the tile and row-
 // tail paths round alike), so the CLS features are those of the full block up to
 // the attention's summation order.
+// Activation of the MX-fp8 c_fc epilogue, whose output is quantised to e4m3 for
+// c_proj: exact GELU (open_clip's nn.GELU) runs in its tanh form there -- its
+// <= 4.8e-4 deviation (2e-4 relative) is far below the e4m3 step (2^-3), and it issues ~9
+// fewer packed VALU ops per element pair than the erf fit (c_fc 0.68 -> 0.59 ms at
+// M = 65792, profiles/r03/configs/mx_epi.jsonl). MICLIP_MX_GELU_ERF=1 keeps erf.
+int mx_act(int act) {
+  static const bool erf = [] {
+    const char* e = getenv("MICLIP_MX_GELU_ERF");
+    return e && atoi(e) != 0;
+  }();
+  return act == ACT_GELU && !erf ? ACT_GELU_TANH : act;
+}
+
 int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, int W, int H,
               int dh, int causal, hipStream_t s, bool cls_only = false) {
   const int M = items * N, dt = m->dtype, r16 = m->resid16;
@@ -385,7 +398,7 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
       MICLIP_HIP(layernorm(dt, w.xc, nullptr, 1, b.ln2_g, b.ln2_b, nullptr, nullptr, items, W, 0,
                            s, r16, w.hq, w.hs));
       MICLIP_HIP(gemm_mx(w.hq, w.hs, b.w_fc, b.s_fc, b.b_fc, w.fq, w.fs, items, 4 * W, W, 5,
-                         m->cfg.act, s));
+                         mx_act(m->cfg.act), s));
       MICLIP_HIP(gemm_mx(w.fq, w.fs, b.w_proj, b.s_proj, b.b_proj, w.xc, nullptr, items, W, 4 * W,
                          1, ACT_NONE, s));
       return 0;
@@ -428,7 +441,7 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
                 mx ? dM * dW + 4 * dW * dW + 4 * dM * dW : gemm_bytes(dM, 4 * dW, dW, 2));
     if (mx)
       MICLIP_HIP(gemm_mx(w.hq, w.hs, b.w_fc, b.s_fc, b.b_fc, w.fq, w.fs, M, 4 * W, W, 5,
-                         m->cfg.act, s));
+                         mx_act(m->cfg.act), s));
     else if (fold)
       MICLIP_HIP(gemm_store_ln(dt, w.x, b.wf_fc, b.c_fc, b.cs_fc, w.stats, w.f, M, 4 * W, W,
                                m->cfg.act, s));

@@ -92,6 +92,21 @@ MICLIP_DEV f32x2 gelu_erf2(f32x2 v) {
 
 constexpr float kQuickGeluK = -1.702f * 1.4426950408889634f;
 
+// GELU, tanh form: x * sigmoid(2 sqrt(2/pi) (x + 0.044715 x^3)) on two values,
+// base 2 with log2(e) folded: t = x (a + b x^2), y = x / (1 + 2^t). Large |x|
+// saturates cleanly (2^t -> inf gives -0, 2^t -> 0 gives x). 2 transcendentals +
+// 5 packed ops per pair against the erf fit's 2 + ~14.
+constexpr float kGeluTanhA = -2.0f * 0.7978845608028654f * 1.4426950408889634f;
+constexpr float kGeluTanhB = kGeluTanhA * 0.044715f;
+MICLIP_DEV f32x2 gelu_tanh2(f32x2 v) {
+  const f32x2 p = __builtin_elementwise_fma(v * v, (f32x2){kGeluTanhB, kGeluTanhB},
+                                            (f32x2){kGeluTanhA, kGeluTanhA});
+  const f32x2 t = v * p;
+  const f32x2 d = (f32x2){__builtin_amdgcn_exp2f(t[0]), __builtin_amdgcn_exp2f(t[1])} +
+                  (f32x2){1.0f, 1.0f};
+  return v * (f32x2){__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+}
+
 // QuickGELU on two values with packed fp32 mul / add (v_pk_mul_f32, v_pk_add_f32):
 // the c_fc epilogue is VALU-bound, and these round exactly like the scalar form.
 MICLIP_DEV f32x2 quick_gelu2(f32x2 v) {

@@ -60,6 +60,10 @@ struct EpiMX {
       const f32x2 lo = gelu_erf2((f32x2){v.x + b.x, v.y + b.y});
       const f32x2 hi = gelu_erf2((f32x2){v.z + b.z, v.w + b.w});
       y = make_float4(lo[0], lo[1], hi[0], hi[1]);
+    } else if constexpr (ACT == ACT_GELU_TANH) {
+      const f32x2 lo = gelu_tanh2((f32x2){v.x + b.x, v.y + b.y});
+      const f32x2 hi = gelu_tanh2((f32x2){v.z + b.z, v.w + b.w});
+      y = make_float4(lo[0], lo[1], hi[0], hi[1]);
     } else {
       y = make_float4(act_fn<ACT>(v.x + b.x), act_fn<ACT>(v.y + b.y), act_fn<ACT>(v.z + b.z),
                       act_fn<ACT>(v.w + b.w));
@@ -409,6 +413,9 @@ hipError_t gemm_mx(const void* A, const void* SA, const void* W, const void* SW,
       if (act == ACT_GELU)
         return launch_mx(A, SA, W, SW, M, N, K,
                          EpiMX<ACT_GELU>{(uint8_t*)C, (uint8_t*)CS, bias, N, N / 128}, s);
+      if (act == ACT_GELU_TANH)
+        return launch_mx(A, SA, W, SW, M, N, K,
+                         EpiMX<ACT_GELU_TANH>{(uint8_t*)C, (uint8_t*)CS, bias, N, N / 128}, s);
       return launch_mx(A, SA, W, SW, M, N, K,
                        EpiMX<ACT_NONE>{(uint8_t*)C, (uint8_t*)CS, bias, N, N / 128}, s);
     default:

@@ -9,7 +9,10 @@
 
 namespace miclip {
 
-enum Act { ACT_NONE = 0, ACT_QUICKGELU = 1, ACT_GELU = 2 };
+// ACT_GELU_TANH: GELU's tanh form, used only where the result is quantised to
+// MX-fp8 next (gemm_mx epi 5): its <= 4.8e-4 deviation from the exact GELU is far
+// below the e4m3 step (2^-3 relative)
+enum Act { ACT_NONE = 0, ACT_QUICKGELU = 1, ACT_GELU = 2, ACT_GELU_TANH = 3 };
 
 // ---- GEMM: C[M,N] = A[M,K] . W[N,K]^T (+ epilogue); A, W in compute dtype ----
 // Shapes: N % 128 == 0, K % 64 == 0, any M >= 1; A, W rows K-contiguous.

@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--ops", default="gemm,attention,layernorm")
     ap.add_argument("--ksweep", action="store_true", help="N=1024 GEMM at K=1024..8192")
     ap.add_argument("--only", default="", help="comma list of gemm shape names to run")
+    ap.add_argument("--attn-variants", default="", help="comma list of attention variants")
     ap.add_argument("--torch", action="store_true", help="also time torch.nn.functional.linear")
     args = ap.parse_args()
     lib = _lib.load_library()
@@ -104,6 +105,8 @@ def main():
         o = torch.empty(M, W, device="cuda", dtype=dt)
 
         avs = (8, 9, 8, 9, 8, 9, 2) if 257 <= args.tokens <= 259 else (0, 1, 0, 1)
+        if args.attn_variants:
+            avs = tuple(int(v) for v in args.attn_variants.split(","))
         for av in (avs if dh == 64 else (0, 0)):
             def fa():
                 rc = lib.miclip_op_attention(0, qkv.data_ptr(), o.data_ptr(), args.batch, args.tokens, H, dh,
