@@ -35,6 +35,8 @@ stamps: $(OBJS)
 	$(HIPCC) $(HIPFLAGS) -fno-honor-nans -fno-slp-vectorize -c scripts/stamps/stamp_attn.hip -o build/stamps/stamp_attn.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) build/stamps/stamp_gemm.o $(filter-out $(OBJ_DIR)/gemm.o,$(OBJS)) -o build/stamps/libstamp_gemm.so
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) build/stamps/stamp_attn.o $(filter-out $(OBJ_DIR)/attention.o,$(OBJS)) -o build/stamps/libstamp_attn.so
+	$(HIPCC) $(HIPFLAGS) -c scripts/stamps/stamp_gemm_kloop.hip -o build/stamps/stamp_gemm_kloop.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) build/stamps/stamp_gemm_kloop.o $(filter-out $(OBJ_DIR)/gemm.o,$(OBJS)) -o build/stamps/libstamp_gemm_kloop.so
 
 clean:
 	rm -rf build $(LIB)

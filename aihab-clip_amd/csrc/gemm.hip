@@ -29,6 +29,17 @@
 #include <cstdlib>
 #include <type_traits>
 
+// MICLIP_STAMPS_KLOOP (scripts/stamps/stamp_gemm_kloop.hip): the persistent
+// kernel's main-loop vmcnt waits get a stamp segment of their own (6; the
+// epilogue's staging-barrier segment then folds into 5)
+#if defined(MICLIP_STAMPS) && defined(MICLIP_STAMPS_KLOOP)
+#define MICLIP_KSTAMP(i) MICLIP_STAMP(i)
+#define MICLIP_ESTAMP(i) MICLIP_STAMP(5)
+#else
+#define MICLIP_KSTAMP(i)
+#define MICLIP_ESTAMP(i) MICLIP_STAMP(i)
+#endif
+
 namespace miclip {
 
 namespace {
@@ -1001,16 +1012,20 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         if (p == 0 && wr == 0 && t > 0) {
+          MICLIP_KSTAMP(1);
           if (t + 1 < nk)
             asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
           else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          MICLIP_KSTAMP(6);
         }
         if (p == 3 && wr == 1 && t + 1 < nk) {
+          MICLIP_KSTAMP(1);
           if (t + 2 < nk)
             asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
           else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          MICLIP_KSTAMP(6);
         }
         const int qi = (p >= 2) ? 1 : 0;
         const int qj = (p == 1 || p == 2) ? 1 : 0;
@@ -1153,7 +1168,7 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         MICLIP_STAMP(5);              // epilogue math + staging writes
         lds_barrier();
-        MICLIP_STAMP(6);              // staging barrier
+        MICLIP_ESTAMP(6);             // staging barrier
         // readback: wave w stores image rows 16w .. 16w+15 in pairs (R, R+1). Lane
         // (h, li) reads the 8 bytes at image half h of both rows (columns 8li + 4h
         // .. +3); one v_permlane32_swap per dword then leaves lanes 0-31 with row R
