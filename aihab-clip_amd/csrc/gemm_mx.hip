@@ -50,6 +50,17 @@ struct EpiMX {
   const float* bias;
   int ldc;
   int kt;  // 128-k tiles per row of the output (= ldc / 128)
+  // act(v) on 4 values, the packed forms put4 uses
+  MICLIP_DEV static float4 act4(float4 v) {
+    if constexpr (ACT == ACT_GELU || ACT == ACT_GELU_TANH || ACT == ACT_QUICKGELU) {
+      const f32x2 a = {v.x, v.y}, b = {v.z, v.w};
+      const f32x2 lo = ACT == ACT_GELU ? gelu_erf2(a) : ACT == ACT_GELU_TANH ? gelu_tanh2(a) : quick_gelu2(a);
+      const f32x2 hi = ACT == ACT_GELU ? gelu_erf2(b) : ACT == ACT_GELU_TANH ? gelu_tanh2(b) : quick_gelu2(b);
+      return make_float4(lo[0], lo[1], hi[0], hi[1]);
+    } else {
+      return v;
+    }
+  }
   MICLIP_DEV float4 bias4(int col) const { return ld_bias4(bias, col); }
   MICLIP_DEV float4 bias4nb(int col) const { return ld_bias4_nb(bias, col); }
   MICLIP_DEV float bias1(int col) const { return bias ? bias[col] : 0.f; }
@@ -90,6 +101,18 @@ MICLIP_DEV void glds4_hidden(const void* g, const void* lds) {
       : "memory");
 }
 
+template <class E> struct IsEpiMX : std::false_type {};
+template <int ACT> struct IsEpiMX<EpiMX<ACT>> : std::true_type {};
+
+// max over the 4 lanes fr, fr + 16, fr + 32, fr + 48 (the 16-lane rows of a wave):
+// one v_permlane16_swap (rows 0<->1, 2<->3) and one v_permlane32_swap
+MICLIP_DEV float max_rows4(float m) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+  m = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
 // The scaled MFMAs have no memory side effects, and without a scheduling
 // fence hipcc sinks all of a K-tile's MFMAs below the phase barriers (every
 // phase's fragments then stay live: 256 VGPRs and spills). sched_barrier(0)
@@ -113,6 +136,10 @@ __global__ __launch_bounds__(512) void gemm256_mx_kernel(const uint8_t* __restri
                                                          int N, int K, Epi epi, int gm) {
   constexpr int HALF = 128 * 128;      // bytes of one half-tile slot
   constexpr int EPI_LD = 260;          // fp32 row stride of the epilogue staging
+  // MX-fp8 output (EpiMX, c_fc -> c_proj): transposed accumulators (operands
+  // swapped, C^T = W . A^T: lane (fk, fr) holds output row fr and 4 consecutive
+  // columns 4fk..), so the 32-column MX blocks are quantised in registers
+  constexpr bool TR = IsEpiMX<Epi>::value;
   constexpr int SCL = 8 * HALF;        // scale ring: 2 x (A 1 KiB + W 1 KiB)
   constexpr int SMEM = 128 * EPI_LD * 4 > SCL + 4096 ? 128 * EPI_LD * 4 : SCL + 4096;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
@@ -198,9 +225,11 @@ __global__ __launch_bounds__(512) void gemm256_mx_kernel(const uint8_t* __restri
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
 #define MICLIP_MXM(IA, IB)                                                                   \
-  acc[qi][qj][i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bf[j],        \
-                                                                       acc[qi][qj][i][j], 0, \
-                                                                       0, IA, sca, IB, scb)
+  acc[qi][qj][i][j] =                                                                        \
+      TR ? __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(bf[j], af[i], acc[qi][qj][i][j],  \
+                                                             0, 0, IB, scb, IA, sca)          \
+         : __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bf[j], acc[qi][qj][i][j],  \
+                                                             0, 0, IA, sca, IB, scb)
         if (j == 0) {
           if (i == 0) MICLIP_MXM(0, 0); else if (i == 1) MICLIP_MXM(1, 0);
           else if (i == 2) MICLIP_MXM(2, 0); else MICLIP_MXM(3, 0);
@@ -261,10 +290,16 @@ __global__ __launch_bounds__(512) void gemm256_mx_kernel(const uint8_t* __restri
         // a plain ds_read here gets a compiler vmcnt(0) in front of it, since
         // hipcc cannot prove the ring disjoint from the in-flight slot DMA.
         const unsigned base = (unsigned)(size_t)(const LDS_AS void*)(smem + SCL + buf * 2048);
+        // early-clobber outputs: without "&" hipcc may give the first read's
+        // destination the second read's address register (it did: ds_read_b64
+        // v[196:197], v196 / ds_read_b32 v207, v197), and whenever the first
+        // read's data landed before the second read issued, the W scales came
+        // from a garbage address -- a timing-dependent wrong K-tile (seen as
+        // run-to-run differences of whole 256-row tiles under two streams)
         u32x2 s2;
         asm volatile(
             "ds_read_b64 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)"
-            : "=v"(s2), "=v"(sb)
+            : "=&v"(s2), "=&v"(sb)
             : "v"(base + soa), "v"(base + sob)
             : "memory");
         sa[0] = s2[0];
@@ -282,6 +317,60 @@ __global__ __launch_bounds__(512) void gemm256_mx_kernel(const uint8_t* __restri
   }
   if (wr == 0) lds_barrier_mx();   // balance the stagger barrier
 
+  if constexpr (TR) {
+    // ---- MX-fp8 epilogue from registers ----
+    // Per (qi, qj, i) a lane holds output row lr = wr*128 + qi*64 + i*16 + fr at
+    // columns c0 + 4fk .. +3 (j = 0) and c0 + 16 + 4fk .. (j = 1), c0 = wc*64 +
+    // qj*32: one 32-column MX block spread over the 4 lanes fr + 16fk. act(acc +
+    // bias), block amax over the 8 values and the 4 lanes, E8M0 exponent, 8 e4m3
+    // bytes -> an LDS image (pitch 272 B: the 16 rows of a ds_write_b32 group hit
+    // distinct 4-bank slots); the tile's 2 KiB of scales -> LDS in the plane's own
+    // order ([128-k tile][k-block 4][row & 15][row >> 4 & 15], mx_scale_index).
+    // Then whole 256-B rows and 16-B scale pieces go out with dwordx4 stores.
+    constexpr int P = 272;
+    uint8_t* img = (uint8_t*)smem;
+    uint8_t* simg = (uint8_t*)smem + 256 * P;
+    lds_barrier_mx();   // every wave is past its last fragment read
+    float4 bq[2][2];
+#pragma unroll
+    for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bq[qj][j] = epi.bias4nb(n0 + wc * 64 + qj * 32 + j * 16 + 4 * fk);
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+      for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int lr = wr * 128 + qi * 64 + i * 16 + fr;
+          const int c0 = wc * 64 + qj * 32;
+          const f32x4 a0 = acc[qi][qj][i][0], a1 = acc[qi][qj][i][1];
+          const float4 y0 = Epi::act4(make_float4(a0[0] + bq[qj][0].x, a0[1] + bq[qj][0].y,
+                                                  a0[2] + bq[qj][0].z, a0[3] + bq[qj][0].w));
+          const float4 y1 = Epi::act4(make_float4(a1[0] + bq[qj][1].x, a1[1] + bq[qj][1].y,
+                                                  a1[2] + bq[qj][1].z, a1[3] + bq[qj][1].w));
+          float am = fmaxf(fmaxf(fmaxf(fabsf(y0.x), fabsf(y0.y)), fmaxf(fabsf(y0.z), fabsf(y0.w))),
+                           fmaxf(fmaxf(fabsf(y1.x), fabsf(y1.y)), fmaxf(fabsf(y1.z), fabsf(y1.w))));
+          const int e = mx_exponent(max_rows4(am));
+          *(unsigned*)(img + lr * P + c0 + 4 * fk) = mx_pack4(y0, e);
+          *(unsigned*)(img + lr * P + c0 + 16 + 4 * fk) = mx_pack4(y1, e);
+          if (fk == 0)
+            simg[(c0 >> 7) * 1024 + ((c0 >> 5) & 3) * 256 + (lr & 15) * 16 + ((lr >> 4) & 15)] =
+                (uint8_t)(e + 127);
+        }
+    lds_barrier_mx();
+    const int ch = tid & 15;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int lr = (tid >> 4) + 32 * k;
+      const u32x4 v = *(const u32x4*)(img + lr * P + ch * 16);
+      if (m0 + lr < M) *(u32x4*)(epi.C + (size_t)(m0 + lr) * epi.ldc + n0 + ch * 16) = v;
+    }
+    if (tid < 128)
+      *(u32x4*)(epi.S + ((size_t)(m0 >> 8) * epi.kt + (n0 >> 7) + (tid >> 6)) * 1024 +
+                (tid & 63) * 16) = *(const u32x4*)(simg + tid * 16);
+    return;
+  }
   // LDS-staged epilogue (as gemm256_kernel): 2 passes of 128 fp32 rows
   float* stg = (float*)smem;
   const int ec = (tid & 63) * 4;
