@@ -37,6 +37,14 @@ namespace {
 
 constexpr float kLog2e = 1.4426950408889634f;
 
+// Eight ones in fp16 / bf16: the head-dim-80 V image's padding chunk 10 (dims
+// 80-87) is DMA'd from here, so the third O^T tile's row 80 accumulates sum_k P
+// (the softmax row sum) in the P.V MFMAs themselves (attend_chunk, DH = 80)
+__device__ __attribute__((aligned(16))) const unsigned short kOnesF16[8] = {
+    0x3C00, 0x3C00, 0x3C00, 0x3C00, 0x3C00, 0x3C00, 0x3C00, 0x3C00};
+__device__ __attribute__((aligned(16))) const unsigned short kOnesBF16[8] = {
+    0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+
 // x (op) x of lane l ^ 32, for every lane: one v_permlane32_swap (gfx950) swaps
 // the upper half of one copy with the lower half of the other, so the pair
 // {r[0], r[1]} is {x_l, x_(l^32)} in some order. A VALU op; __shfl_xor(x, 32)
@@ -177,12 +185,16 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
     for (int r = 0; r < 16; ++r) {
       const float v = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[r], c2, -m));
       sacc[r] = v;
-      if (r < 4)
-        ps[r] = v;
-      else
-        ps[r & 3] += v;
+      if constexpr (DH != 80) {
+        if (r < 4)
+          ps[r] = v;
+        else
+          ps[r & 3] += v;
+      }
     }
-    lsum += (ps[0] + ps[2]) + (ps[1] + ps[3]);   // the former packed pairs' order
+    // head dim 80: the row sum rides the P.V MFMAs (V's padding dims 80-87 are
+    // ones: O^T rows 80-87 = sum_k P, rescaled with O) -- 16 fewer adds per tile
+    if constexpr (DH != 80) lsum += (ps[0] + ps[2]) + (ps[1] + ps[3]);   // the former packed pairs' order
     // ---- P^T as B operand: k-step s2 uses accumulator regs 8*s2 .. 8*s2+7 ----
     i16x8 pf[2];
 #pragma unroll
@@ -225,7 +237,13 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
       softmax_pv(kt, sa);
     }
   }
-  if (last) lsum = xor32_sum(lsum);
+  if constexpr (DH == 80) {
+    // O^T row 80 (hh = 0 lanes) / 84 (hh = 1): both in the ones chunk, so every
+    // lane holds its query's sum of the P values the MFMAs used
+    if (last) lsum = o[2][8];
+  } else {
+    if (last) lsum = xor32_sum(lsum);
+  }
 }
 
 // Keys [key0, key0 + nkeys) (at most a few: the keys past the last full 32-key
@@ -386,16 +404,33 @@ __global__ __launch_bounds__(DH == 64 ? 640 : 576) void attention_kernel(
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else {
-    for (int idx = threadIdx.x; idx < Npad * G::CH; idx += blockDim.x) {
-      const int row = idx / G::CH, c = idx - row * G::CH;
-      i16x8 kv = {0, 0, 0, 0, 0, 0, 0, 0}, vv = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (row < N && c * 8 < DH) {
-        kv = *(const i16x8*)(base + (size_t)row * ld + D + c * 8);
-        vv = *(const i16x8*)(base + (size_t)row * ld + 2 * D + c * 8);
+    // head dim 80: the same all-DMAs-then-one-wait staging over 192-B rows. A
+    // 1-KiB piece covers 5 1/3 rows, so each lane finds the (row, physical chunk)
+    // its 16 bytes land on and fetches the logical chunk there (the swizzle is an
+    // involution: swz(swz(c, x), x) == c). Padding chunks (dims 80-95) take dims
+    // 16-31 of the same row -- finite; K's are never read (5 k-steps cover dims
+    // 0-79), V's only feed O^T rows 80-95, which are never stored. Pad rows repeat
+    // row N - 1. (The register path this replaces loaded 2 x 16 B per thread and
+    // waited before each LDS write: 6 serial round trips per head at N = 257.)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    const int pieces = Npad * G::ROWB / 1024;   // Npad % 32 == 0: whole pieces
+    for (int pc = wave; pc < 2 * pieces; pc += nwv) {
+      const bool isv = pc >= pieces;
+      const int piece = isv ? pc - pieces : pc;
+      const int off = piece * 1024 + lane * 16;
+      const int row = off / G::ROWB, pch = (off - row * G::ROWB) >> 4;
+      int c = G::swz(pch, isv ? ((row & 3) << 1) : ((row >> 1) & 7));
+      const T* src;
+      if (isv && c == DH / 8) {   // V dims 80-87: ones (the row sum, see kOnesF16)
+        src = (const T*)(std::is_same_v<T, _Float16> ? kOnesF16 : kOnesBF16);
+      } else {
+        if (c * 8 >= DH) c -= 8;
+        const int r = row < N ? row : N - 1;
+        src = base + (size_t)r * ld + (isv ? 2 * D : D) + c * 8;
       }
-      *(i16x8*)(kimg + row * G::ROWB + (G::swz(c, (row >> 1) & 7) << 4)) = kv;
-      *(i16x8*)(vimg + row * G::ROWB + (G::swz(c, (row & 3) << 1) << 4)) = vv;
+      glds16_hidden(src, (isv ? vimg : kimg) + piece * 1024);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
 

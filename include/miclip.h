@@ -42,7 +42,10 @@ enum miclip_status {
  * rest as MICLIP_FP16. SURVEY §8f row 4 (C5 fp8 weights); parity unpinned. */
 /* MICLIP_F32: an input element type only (miclip_encode_image_ex images). */
 enum miclip_dtype { MICLIP_FP16 = 0, MICLIP_BF16 = 1, MICLIP_MXFP8 = 2, MICLIP_F32 = 3 };
-enum miclip_act { MICLIP_ACT_QUICKGELU = 1, MICLIP_ACT_GELU = 2 };
+/* MICLIP_ACT_GELU_TANH: GELU's tanh form, accepted by the op-level MX-fp8 GEMM
+ * (miclip_op_gemm_mx epi 5) -- the model's MX c_fc uses it where its output is
+ * quantised to e4m3; a model config's act is QUICKGELU or GELU */
+enum miclip_act { MICLIP_ACT_QUICKGELU = 1, MICLIP_ACT_GELU = 2, MICLIP_ACT_GELU_TANH = 3 };
 
 /* encode_image flags */
 #define MICLIP_FLAG_NORMALIZE 1u  /* F.normalize(feats, dim=-1): aihab_utils/feature_cache.py:126-127 */
