@@ -77,7 +77,7 @@ struct Block {
   float* b_proj = nullptr;
   float *ln1_g = nullptr, *ln1_b = nullptr, *ln2_g = nullptr, *ln2_b = nullptr;
   // MX-fp8 models: scale planes of w_qkv / w_fc / w_proj (which then hold e4m3 bytes)
-  void *s_qkv = nullptr, *s_fc = nullptr, *s_proj = nullptr;
+  void *s_qkv = nullptr, *s_fc = nullptr, *s_proj = nullptr, *s_out = nullptr;
   // folded LayerNorm (miclip_model::lnfold): W diag(gamma) of QKV / c_fc, their
   // column sums and folded biases (epilogue.h EpiStoreLN)
   void *wf_qkv = nullptr, *wf_fc = nullptr;
@@ -116,6 +116,14 @@ struct miclip_model {
   // MICLIP_MXFP8: QKV / c_fc / c_proj run on MX-fp8 operands (gemm_mx.hip);
   // everything else (patch embed, attention, out-proj, stream) as fp16 compute.
   bool mx = false;
+  // MX-fp8 models: the VISION tower's attention out-projection on MX-fp8 too (the
+  // attention output quantised by quant_mx: 80-wide heads straddle the 32-wide
+  // blocks, so no attention epilogue can); MICLIP_MX_OUT=0 at model creation keeps
+  // it fp16. The text tower keeps fp16 out-proj: there the extra quantisation
+  // raised the text 1-cos from 4.5e-3 to 6.9e-3 (tolerance 1e-2) for a path the
+  // benchmarks do not time; in the vision tower image 1-cos moved 4.90e-4 ->
+  // 4.96e-4 for +1.0 % (C5, same box: profiles/r03/configs/mx_out_ab.txt)
+  bool mx_out = false;
   // ln_1 / ln_2 folded into the QKV / c_fc GEMMs (fp16 stream models;
   // MICLIP_LN_FOLD=0 runs the LayerNorm kernels instead); folded weights are
   // rebuilt per tower after every weight load
@@ -218,7 +226,8 @@ void add_block_slots(miclip_model* m, const std::string& prefix, Block& b, int W
   add_slot(m, prefix + "attn.in_proj_weight", &b.w_qkv, (int64_t)3 * W * W, 1, visual,
            m->mx ? &b.s_qkv : nullptr);
   add_slot(m, prefix + "attn.in_proj_bias", (void**)&b.b_qkv, 3 * W, 0, visual);
-  add_slot(m, prefix + "attn.out_proj.weight", &b.w_out, (int64_t)W * W, 1, visual);
+  add_slot(m, prefix + "attn.out_proj.weight", &b.w_out, (int64_t)W * W, 1, visual,
+           m->mx_out && visual ? &b.s_out : nullptr);
   add_slot(m, prefix + "attn.out_proj.bias", (void**)&b.b_out, W, 0, visual);
   add_slot(m, prefix + "ln_1.weight", (void**)&b.ln1_g, W, 0, visual);
   add_slot(m, prefix + "ln_1.bias", (void**)&b.ln1_b, W, 0, visual);
@@ -393,7 +402,13 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
                 dM * 2 * dW * 2 + 10 * dW * dW * 2);
     MICLIP_HIP(attention_q0(dt, w.qkv, w.o, items, N, H, s, dh));
     MICLIP_HIP(gather_rows(w.x, w.xc, items, N, W, r16 ? 2 : 4, s));
-    MICLIP_HIP(gemm_residual(dt, w.o, b.w_out, b.b_out, w.xc, items, W, W, s, 0, r16));
+    if (b.s_out) {   // MX-fp8 out-proj (vision tower of an MX model)
+      MICLIP_HIP(quant_mx(1, w.o, items, W, w.hq, w.hs, s));
+      MICLIP_HIP(gemm_mx(w.hq, w.hs, b.w_out, b.s_out, b.b_out, w.xc, nullptr, items, W, W, 1,
+                         ACT_NONE, s));
+    } else {
+      MICLIP_HIP(gemm_residual(dt, w.o, b.w_out, b.b_out, w.xc, items, W, W, s, 0, r16));
+    }
     if (mx) {   // MX-fp8 MLP on the CLS rows (their scale blocks are row-local)
       MICLIP_HIP(layernorm(dt, w.xc, nullptr, 1, b.ln2_g, b.ln2_b, nullptr, nullptr, items, W, 0,
                            s, r16, w.hq, w.hs));
@@ -422,7 +437,13 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
   }
   {
     ProfScope p(m, K_GEMM_OUT, s, gemm_flops(dM, dW, dW), gemm_bytes(dM, dW, dW, 2 * rb));
-    MICLIP_HIP(gemm_residual(dt, w.o, b.w_out, b.b_out, w.x, M, W, W, s, 0, r16));
+    if (b.s_out) {   // quantise the attention output (hq / hs are free here), MX GEMM
+      MICLIP_HIP(quant_mx(1, w.o, M, W, w.hq, w.hs, s));
+      MICLIP_HIP(gemm_mx(w.hq, w.hs, b.w_out, b.s_out, b.b_out, w.x, nullptr, M, W, W, 1,
+                         ACT_NONE, s));
+    } else {
+      MICLIP_HIP(gemm_residual(dt, w.o, b.w_out, b.b_out, w.x, M, W, W, s, 0, r16));
+    }
   }
   if (fold) {
     ProfScope p(m, K_LAYERNORM, s, 0, dM * (dW * rb + 8));
@@ -613,6 +634,10 @@ int miclip_model_create(const miclip_config* cfg, int device, miclip_model** out
   m->cfg = c;
   m->device = device;
   m->mx = cfg->compute_dtype == MICLIP_MXFP8;
+  {
+    const char* e = getenv("MICLIP_MX_OUT");
+    m->mx_out = m->mx && !(e && atoi(e) == 0);
+  }
   m->dtype = m->mx ? MICLIP_FP16 : cfg->compute_dtype;   // the fp16 kernels' operand type
   {
     const char* e = getenv("MICLIP_RESID_F32");
