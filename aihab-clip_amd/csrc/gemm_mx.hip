@@ -103,6 +103,9 @@ MICLIP_DEV void glds4_hidden(const void* g, const void* lds) {
 
 template <class E> struct IsEpiMX : std::false_type {};
 template <int ACT> struct IsEpiMX<EpiMX<ACT>> : std::true_type {};
+// fp16 store epilogues (the MX QKV GEMM) also run on transposed accumulators
+template <class E> struct IsEpiStoreH : std::false_type {};
+template <int ACT> struct IsEpiStoreH<EpiStore<_Float16, ACT>> : std::true_type {};
 
 // max over the 4 lanes fr, fr + 16, fr + 32, fr + 48 (the 16-lane rows of a wave):
 // one v_permlane16_swap (rows 0<->1, 2<->3) and one v_permlane32_swap
@@ -139,7 +142,7 @@ __global__ __launch_bounds__(512) void gemm256_mx_kernel(const uint8_t* __restri
   // MX-fp8 output (EpiMX, c_fc -> c_proj): transposed accumulators (operands
   // swapped, C^T = W . A^T: lane (fk, fr) holds output row fr and 4 consecutive
   // columns 4fk..), so the 32-column MX blocks are quantised in registers
-  constexpr bool TR = IsEpiMX<Epi>::value;
+  constexpr bool TR = IsEpiMX<Epi>::value || IsEpiStoreH<Epi>::value;
   constexpr int SCL = 8 * HALF;        // scale ring: 2 x (A 1 KiB + W 1 KiB)
   constexpr int SMEM = 128 * EPI_LD * 4 > SCL + 4096 ? 128 * EPI_LD * 4 : SCL + 4096;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
@@ -317,7 +320,59 @@ __global__ __launch_bounds__(512) void gemm256_mx_kernel(const uint8_t* __restri
   }
   if (wr == 0) lds_barrier_mx();   // balance the stagger barrier
 
-  if constexpr (TR) {
+  if constexpr (IsEpiStoreH<Epi>::value) {
+    // ---- fp16 store from transposed accumulators (gemm.hip gemm256s_kernel's TR
+    // store epilogue in one pass of 256 rows): val4 in registers, the 8 output
+    // bytes into a row-major fp16 image (pitch 520 B, each row's even and odd 8-B
+    // column quads in separate 256-B halves), then per row pair one ds_read_b64 per
+    // half and a v_permlane32_swap per dword give each half-wave one whole 512-B
+    // row segment to store
+    constexpr int TLD = 520;
+    char* img = smem;
+    lds_barrier_mx();   // every wave is past its last fragment read
+    float4 tb[2][2];
+#pragma unroll
+    for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) tb[qj][j] = epi.bias4nb(n0 + (wc * 16 + qj * 8 + j * 4 + fk) * 4);
+#pragma unroll
+    for (int qi = 0; qi < 2; ++qi)
+#pragma unroll
+      for (int qj = 0; qj < 2; ++qj)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int ir = wr * 128 + qi * 64 + i * 16 + fr;
+            const int c4 = wc * 16 + qj * 8 + j * 4 + fk;
+            const f32x4 a = acc[qi][qj][i][j];
+            *(i16x4*)(img + ir * TLD + (c4 & 1) * 256 + (c4 >> 1) * 8) =
+                epi.val4(make_float4(a[0], a[1], a[2], a[3]), tb[qj][j]);
+          }
+    lds_barrier_mx();
+    const int h = lane >> 5, li = lane & 31;
+#pragma unroll
+    for (int p0 = 0; p0 < 16; p0 += 2) {
+      i16x4 va[2], vb[2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int R = wave * 32 + 2 * (p0 + p);
+        va[p] = *(const i16x4*)(img + R * TLD + h * 256 + li * 8);
+        vb[p] = *(const i16x4*)(img + (R + 1) * TLD + h * 256 + li * 8);
+      }
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const u32x2 a = __builtin_bit_cast(u32x2, va[p]), b = __builtin_bit_cast(u32x2, vb[p]);
+        const auto s0 = __builtin_amdgcn_permlane32_swap(a[0], b[0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane32_swap(a[1], b[1], false, false);
+        const u32x4 w = {s0[0], s1[0], s0[1], s1[1]};
+        const int row = m0 + wave * 32 + 2 * (p0 + p) + h;
+        if (row < M) *(u32x4*)(epi.C + (size_t)row * epi.ldc + n0 + li * 8) = w;
+      }
+    }
+    return;
+  }
+  if constexpr (IsEpiMX<Epi>::value) {
     // ---- MX-fp8 epilogue from registers ----
     // Per (qi, qj, i) a lane holds output row lr = wr*128 + qi*64 + i*16 + fr at
     // columns c0 + 4fk .. +3 (j = 0) and c0 + 16 + 4fk .. (j = 1), c0 = wc*64 +
