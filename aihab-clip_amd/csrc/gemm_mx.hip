@@ -106,6 +106,7 @@ template <int ACT> struct IsEpiMX<EpiMX<ACT>> : std::true_type {};
 // fp16 store epilogues (the MX QKV GEMM) also run on transposed accumulators
 template <class E> struct IsEpiStoreH : std::false_type {};
 template <int ACT> struct IsEpiStoreH<EpiStore<_Float16, ACT>> : std::true_type {};
+template <> struct IsEpiStoreH<EpiResidual<_Float16>> : std::true_type {};   // + x at readback
 
 // max over the 4 lanes fr, fr + 16, fr + 32, fr + 48 (the 16-lane rows of a wave):
 // one v_permlane16_swap (rows 0<->1, 2<->3) and one v_permlane32_swap
@@ -326,7 +327,10 @@ __global__ __launch_bounds__(512) void gemm256_mx_kernel(const uint8_t* __restri
     // bytes into a row-major fp16 image (pitch 520 B, each row's even and odd 8-B
     // column quads in separate 256-B halves), then per row pair one ds_read_b64 per
     // half and a v_permlane32_swap per dword give each half-wave one whole 512-B
-    // row segment to store
+    // row segment to store. The fp16 residual (EpiResidual, c_proj / out-proj):
+    // val4 is t = fp16(acc + bias); each lane loads its 16 x pieces (16 B, the
+    // readback layout) after staging and adds x + t with packed fp16 adds at
+    // readback -- the reference's two roundings, as the fp16 kernels do
     constexpr int TLD = 520;
     char* img = smem;
     lds_barrier_mx();   // every wave is past its last fragment read
@@ -349,8 +353,26 @@ __global__ __launch_bounds__(512) void gemm256_mx_kernel(const uint8_t* __restri
             *(i16x4*)(img + ir * TLD + (c4 & 1) * 256 + (c4 >> 1) * 8) =
                 epi.val4(make_float4(a[0], a[1], a[2], a[3]), tb[qj][j]);
           }
-    lds_barrier_mx();
     const int h = lane >> 5, li = lane & 31;
+    constexpr bool RES = PrefetchX<Epi>::value;
+    _Float16* cb;
+    int cld;
+    if constexpr (RES) {
+      cb = epi.X;
+      cld = epi.ldx;
+    } else {
+      cb = epi.C;
+      cld = epi.ldc;
+    }
+    u32x4 xq[16];
+    if constexpr (RES) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int row = m0 + wave * 32 + 2 * k + h;
+        xq[k] = *(const u32x4*)(cb + (size_t)(row < M ? row : M - 1) * cld + n0 + li * 8);
+      }
+    }
+    lds_barrier_mx();
 #pragma unroll
     for (int p0 = 0; p0 < 16; p0 += 2) {
       i16x4 va[2], vb[2];
@@ -365,9 +387,15 @@ __global__ __launch_bounds__(512) void gemm256_mx_kernel(const uint8_t* __restri
         const u32x2 a = __builtin_bit_cast(u32x2, va[p]), b = __builtin_bit_cast(u32x2, vb[p]);
         const auto s0 = __builtin_amdgcn_permlane32_swap(a[0], b[0], false, false);
         const auto s1 = __builtin_amdgcn_permlane32_swap(a[1], b[1], false, false);
-        const u32x4 w = {s0[0], s1[0], s0[1], s1[1]};
+        u32x4 w = {s0[0], s1[0], s0[1], s1[1]};
+        if constexpr (RES) {   // x + t, 8 fp16 pairs of adds
+          unsigned t[4] = {w[0], w[1], w[2], w[3]};
+          const unsigned x[4] = {xq[p0 + p][0], xq[p0 + p][1], xq[p0 + p][2], xq[p0 + p][3]};
+          Epi::template add_x<4>(t, x);
+          w = (u32x4){t[0], t[1], t[2], t[3]};
+        }
         const int row = m0 + wave * 32 + 2 * (p0 + p) + h;
-        if (row < M) *(u32x4*)(epi.C + (size_t)row * epi.ldc + n0 + li * 8) = w;
+        if (row < M) *(u32x4*)(cb + (size_t)row * cld + n0 + li * 8) = w;
       }
     }
     return;
