@@ -121,6 +121,11 @@ MICLIP_DEV float half_sum(float x) {
 
 // MX = true: MX-fp8 output (the fp8 GEMM's A operand) instead of T; a 32-value
 // block is the 4 lanes of a quad here (8 values per lane), scale by lane 0 of it.
+// A workgroup takes kLnRows consecutive rows (each wave kLnRows / 4, two at a
+// time): gamma / beta are staged in LDS once per workgroup instead of being
+// re-loaded (4 x 16 B per lane per 256 columns) for every row pair.
+constexpr int kLnRows = 32;
+
 template <int NI, typename T, bool MX>
 __global__ __launch_bounds__(256) void layernorm_h2_kernel(const _Float16* in,  // may alias out
                                                            const float* __restrict__ gamma,
@@ -128,59 +133,70 @@ __global__ __launch_bounds__(256) void layernorm_h2_kernel(const _Float16* in,  
                                                            T* out, int R, int D,
                                                            uint8_t* __restrict__ oq,
                                                            uint8_t* __restrict__ os) {
-  const int lane = threadIdx.x & 63, hl = lane & 31;
-  const int r = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
-  if ((blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 >= R) return;   // whole wave past the end
-  const bool valid = r < R;
-  const _Float16* src = in + (size_t)(valid ? r : R - 1) * D + hl * 8;
-  float v[NI][8];
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const i16x8 h = *(const i16x8*)(src + i * 256);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[i][e] = from_bits<_Float16>(h[e]);
-    s += ((v[i][0] + v[i][1]) + (v[i][2] + v[i][3])) + ((v[i][4] + v[i][5]) + (v[i][6] + v[i][7]));
+  __shared__ float4 gb[2][NI * 64];
+  for (int t = threadIdx.x; t < NI * 64; t += 256) {
+    gb[0][t] = ((const float4*)gamma)[t];
+    gb[1][t] = ((const float4*)beta)[t];
   }
-  const float mean = half_sum(s) / (float)D;
-  float q = 0.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, hl = lane & 31;
+  const int wave = threadIdx.x >> 6;
+  constexpr int PAIRS = kLnRows / 8;   // row pairs per wave
+  for (int it = 0; it < PAIRS; ++it) {
+    const int p2 = ((blockIdx.x * 4 + wave) * PAIRS + it) * 2;   // first row of the pair
+    if (p2 >= R) break;                                          // wave-uniform
+    const int r = p2 + (lane >> 5);
+    const bool valid = r < R;
+    const _Float16* src = in + (size_t)(valid ? r : R - 1) * D + hl * 8;
+    float v[NI][8];
+    float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < NI; ++i)
+    for (int i = 0; i < NI; ++i) {
+      const i16x8 h = *(const i16x8*)(src + i * 256);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      v[i][e] -= mean;
-      q += v[i][e] * v[i][e];
+      for (int e = 0; e < 8; ++e) v[i][e] = from_bits<_Float16>(h[e]);
+      s += ((v[i][0] + v[i][1]) + (v[i][2] + v[i][3])) + ((v[i][4] + v[i][5]) + (v[i][6] + v[i][7]));
     }
-  const float rstd = rsqrtf(half_sum(q) / (float)D + 1e-5f);
+    const float mean = half_sum(s) / (float)D;
+    float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int c = i * 256 + hl * 8;
-    const float4 g0 = *(const float4*)(gamma + c), g1 = *(const float4*)(gamma + c + 4);
-    const float4 b0 = *(const float4*)(beta + c), b1 = *(const float4*)(beta + c + 4);
-    const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
-    const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-    if constexpr (MX) {
-      float y[8];
-      float a = 0.f;
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        y[e] = v[i][e] * rstd * g[e] + b[e];
-        a = fmaxf(a, fabsf(y[e]));
+        v[i][e] -= mean;
+        q += v[i][e] * v[i][e];
       }
-      a = fmaxf(a, dppf<0xB1>(a));   // quad_perm [1,0,3,2]
-      a = fmaxf(a, dppf<0x4E>(a));   // quad_perm [2,3,0,1]: the quad's 32 values
-      const int ex = mx_exponent(a);
-      const unsigned lo = mx_pack4(make_float4(y[0], y[1], y[2], y[3]), ex);
-      const unsigned hi = mx_pack4(make_float4(y[4], y[5], y[6], y[7]), ex);
-      if (valid) {
-        *(uint2*)(oq + (size_t)r * D + c) = make_uint2(lo, hi);
-        if ((hl & 3) == 0) os[mx_scale_index(r, c >> 5, D / 128)] = (uint8_t)(ex + 127);
-      }
-    } else {
-      i16x8 o;
+    const float rstd = rsqrtf(half_sum(q) / (float)D + 1e-5f);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = to_bits<T>(v[i][e] * rstd * g[e] + b[e]);
-      if (valid) *(i16x8*)(out + (size_t)r * D + c) = o;
+    for (int i = 0; i < NI; ++i) {
+      const int c = i * 256 + hl * 8;
+      const float4 g0 = gb[0][c / 4], g1 = gb[0][c / 4 + 1];
+      const float4 b0 = gb[1][c / 4], b1 = gb[1][c / 4 + 1];
+      const float g[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      if constexpr (MX) {
+        float y[8];
+        float a = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          y[e] = v[i][e] * rstd * g[e] + b[e];
+          a = fmaxf(a, fabsf(y[e]));
+        }
+        a = fmaxf(a, dppf<0xB1>(a));   // quad_perm [1,0,3,2]
+        a = fmaxf(a, dppf<0x4E>(a));   // quad_perm [2,3,0,1]: the quad's 32 values
+        const int ex = mx_exponent(a);
+        const unsigned lo = mx_pack4(make_float4(y[0], y[1], y[2], y[3]), ex);
+        const unsigned hi = mx_pack4(make_float4(y[4], y[5], y[6], y[7]), ex);
+        if (valid) {
+          *(uint2*)(oq + (size_t)r * D + c) = make_uint2(lo, hi);
+          if ((hl & 3) == 0) os[mx_scale_index(r, c >> 5, D / 128)] = (uint8_t)(ex + 127);
+        }
+      } else {
+        i16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = to_bits<T>(v[i][e] * rstd * g[e] + b[e]);
+        if (valid) *(i16x8*)(out + (size_t)r * D + c) = o;
+      }
     }
   }
 }
@@ -291,7 +307,7 @@ __global__ __launch_bounds__(256) void ln_fold_kernel(const T* __restrict__ W,
 template <typename T, bool MX = false>
 hipError_t ln_h2_dispatch(const _Float16* in, const float* g, const float* b, void* out, int R,
                           int D, hipStream_t s, void* oq = nullptr, void* os = nullptr) {
-  const dim3 grid((R + 7) / 8), block(256);
+  const dim3 grid((R + kLnRows - 1) / kLnRows), block(256);
 #define MICLIP_LNH_CASE(V)                                                                     \
   case V:                                                                                      \
     hipLaunchKernelGGL((layernorm_h2_kernel<V, T, MX>), grid, block, 0, s, in, g, b, (T*)out, \
