@@ -535,6 +535,41 @@ __global__ __launch_bounds__(256) void quant_mx_kernel(const TI* __restrict__ in
   if ((lane & 7) == 0) sc[mx_scale_index(r, k >> 5, K / 128)] = (uint8_t)(e + 127);
 }
 
+// fp16 rows -> MX-fp8, 16-B loads: a lane takes 8 consecutive k, a 32-block is a
+// quad (max by two DPP steps), each thread 2 chunks. R * K / 8 is a multiple of 4,
+// so a quad is either wholly in range or wholly past the end.
+__global__ __launch_bounds__(256) void quant_mx_h8_kernel(const _Float16* __restrict__ in,
+                                                          size_t chunks, int K,
+                                                          uint8_t* __restrict__ q,
+                                                          uint8_t* __restrict__ sc) {
+  const int kc = K / 8;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const size_t c = ((size_t)blockIdx.x * 2 + u) * 256 + threadIdx.x;
+    const bool valid = c < chunks;
+    const i16x8 h = *(const i16x8*)(in + (valid ? c : 0) * 8);
+    float y[8];
+    float a = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      y[e] = from_bits<_Float16>(h[e]);
+      a = fmaxf(a, fabsf(y[e]));
+    }
+    a = fmaxf(a, dppf<0xB1>(a));   // quad_perm [1,0,3,2]
+    a = fmaxf(a, dppf<0x4E>(a));   // quad_perm [2,3,0,1]
+    const int ex = mx_exponent(a);
+    const unsigned lo = mx_pack4(make_float4(y[0], y[1], y[2], y[3]), ex);
+    const unsigned hi = mx_pack4(make_float4(y[4], y[5], y[6], y[7]), ex);
+    if (valid) {
+      *(uint2*)(q + c * 8) = make_uint2(lo, hi);
+      if ((threadIdx.x & 3) == 0) {
+        const int r = (int)(c / kc), k = (int)(c - (size_t)r * kc) * 8;
+        sc[mx_scale_index(r, k >> 5, K / 128)] = (uint8_t)(ex + 127);
+      }
+    }
+  }
+}
+
 template <class Epi>
 hipError_t launch_mx(const void* A, const void* SA, const void* W, const void* SW, int M, int N,
                      int K, Epi epi, hipStream_t s) {
@@ -554,7 +589,11 @@ size_t mx_scale_bytes(int rows, int K) { return (size_t)((rows + 255) / 256) * (
 hipError_t quant_mx(int in_f16, const void* in, int R, int K, void* q, void* sc, hipStream_t s) {
   if (R < 1 || K % 256) return hipErrorInvalidValue;
   const int segs = R * (K / 256);
-  if (in_f16)
+  if (in_f16 && !getenv("MICLIP_QUANT_MX_W4")) {
+    const size_t chunks = (size_t)R * (K / 8);
+    hipLaunchKernelGGL(quant_mx_h8_kernel, dim3((unsigned)((chunks + 511) / 512)), dim3(256), 0, s,
+                       (const _Float16*)in, chunks, K, (uint8_t*)q, (uint8_t*)sc);
+  } else if (in_f16)
     hipLaunchKernelGGL(quant_mx_kernel<_Float16>, dim3((segs + 3) / 4), dim3(256), 0, s,
                        (const _Float16*)in, R, K, (uint8_t*)q, (uint8_t*)sc);
   else
