@@ -177,3 +177,30 @@ def test_layernorm_mx(lib, R, D, in_f16):
     step = np.ldexp(1.0, E_ref).repeat(32, axis=1)
     assert np.all(np.abs(deq - y) <= np.abs(y) * 2.0 ** -3 + step * 2.0 ** -8)
     assert (q.cpu().numpy() == q_ref).mean() > 0.99
+
+
+def test_quant_mx_f16_full_size_matches_lane8_kernel(lib, monkeypatch):
+    """ViT-H/14 bs=256 attention output (65 792 x 1280 fp16): the 16-B-load quantiser
+    (default) is byte-identical to the 8-lane-block kernel (MICLIP_QUANT_MX_W4=1),
+    scales included, at the full size the oracle is too slow for."""
+    R, K = 65792, 1280
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randn(R, K, device="cuda", generator=g)
+    x *= torch.exp2(torch.randint(-6, 7, (R, K // 32), device="cuda", generator=g).float()).repeat_interleave(32, 1)
+    x[0, :32] = 0
+    x[R - 1, 64:96] = 0
+    x[R - 1, 70] = -300.0
+    xh = x.half()
+
+    def run():
+        q = torch.empty(R, K, dtype=torch.uint8, device="cuda")
+        s = torch.zeros(int(lib.miclip_mx_scale_bytes(R, K)), dtype=torch.uint8, device="cuda")
+        _check(lib, lib.miclip_op_quant_mx(xh.data_ptr(), 1, R, K, q.data_ptr(), s.data_ptr(), _stream()))
+        torch.cuda.synchronize()
+        return q, s
+
+    q8, s8 = run()
+    monkeypatch.setenv("MICLIP_QUANT_MX_W4", "1")
+    q4, s4 = run()
+    assert torch.equal(q8, q4)
+    assert torch.equal(s8, s4)
