@@ -223,8 +223,12 @@ void add_slot(miclip_model* m, const std::string& name, void** dst, int64_t nume
 }
 
 void add_block_slots(miclip_model* m, const std::string& prefix, Block& b, int W, bool visual) {
+  // MX-fp8 operands in the VISION tower only: the text tower is one classifier's
+  // prompts per run (no throughput reason for fp8), and on MX its 1-cos was
+  // 4.5e-3 against the north star's 1e-3, so it runs the fp16 kernels
+  const bool mx = m->mx && visual;
   add_slot(m, prefix + "attn.in_proj_weight", &b.w_qkv, (int64_t)3 * W * W, 1, visual,
-           m->mx ? &b.s_qkv : nullptr);
+           mx ? &b.s_qkv : nullptr);
   add_slot(m, prefix + "attn.in_proj_bias", (void**)&b.b_qkv, 3 * W, 0, visual);
   add_slot(m, prefix + "attn.out_proj.weight", &b.w_out, (int64_t)W * W, 1, visual,
            m->mx_out && visual ? &b.s_out : nullptr);
@@ -232,10 +236,10 @@ void add_block_slots(miclip_model* m, const std::string& prefix, Block& b, int W
   add_slot(m, prefix + "ln_1.weight", (void**)&b.ln1_g, W, 0, visual);
   add_slot(m, prefix + "ln_1.bias", (void**)&b.ln1_b, W, 0, visual);
   add_slot(m, prefix + "mlp.c_fc.weight", &b.w_fc, (int64_t)4 * W * W, 1, visual,
-           m->mx ? &b.s_fc : nullptr);
+           mx ? &b.s_fc : nullptr);
   add_slot(m, prefix + "mlp.c_fc.bias", (void**)&b.b_fc, 4 * W, 0, visual);
   add_slot(m, prefix + "mlp.c_proj.weight", &b.w_proj, (int64_t)4 * W * W, 1, visual,
-           m->mx ? &b.s_proj : nullptr);
+           mx ? &b.s_proj : nullptr);
   add_slot(m, prefix + "mlp.c_proj.bias", (void**)&b.b_proj, W, 0, visual);
   add_slot(m, prefix + "ln_2.weight", (void**)&b.ln2_g, W, 0, visual);
   add_slot(m, prefix + "ln_2.bias", (void**)&b.ln2_b, W, 0, visual);
@@ -293,7 +297,7 @@ int ensure_ws(miclip_model* m, Workspace& w, int items, int ntok, int W, bool im
   if ((rc = dev_alloc(m, &w.qkv, (size_t)rows * 3 * W * e))) return rc;
   if ((rc = dev_alloc(m, &w.o, (size_t)rows * W * e))) return rc;
   if ((rc = dev_alloc(m, &w.f, (size_t)rows * 4 * W * e))) return rc;
-  if (m->mx) {
+  if (m->mx && image) {
     // scale planes: + 4 blocks of 256 rows so that every batch-split window
     // (view) starts on its own 256-row block
     if ((rc = dev_alloc(m, &w.hq, (size_t)rows * W))) return rc;
@@ -369,7 +373,7 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
               int dh, int causal, hipStream_t s, bool cls_only = false) {
   const int M = items * N, dt = m->dtype, r16 = m->resid16;
   const double dM = M, dW = W, rb = r16 ? 2 : 4;  // residual bytes per element
-  const bool mx = m->mx;   // MX-fp8 operands for QKV / c_fc / c_proj
+  const bool mx = b.s_qkv != nullptr;   // MX-fp8 operands for QKV / c_fc / c_proj (vision)
   const bool fold = m->lnfold && b.wf_qkv;
   if (fold) {
     ProfScope p(m, K_LAYERNORM, s, 0, dM * (dW * rb + 8));

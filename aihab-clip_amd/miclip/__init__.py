@@ -28,7 +28,8 @@ def _transform(n_px):
 
 
 def load(name, device="cuda" if torch.cuda.is_available() else "cpu", jit=False,
-         download_root=None, *, seed: int = 0, compute_dtype: str = "fp16", surface=None):
+         download_root=None, *, seed: int = 0, compute_dtype: str = "fp16", surface=None,
+         config=None):
     """Counterpart of clip.load (clip/clip.py:89-137): returns (state_dict, model, preprocess).
 
     `name` is a model name from available_models() -- resolved offline to the
@@ -41,6 +42,11 @@ def load(name, device="cuda" if torch.cuda.is_available() else "cpu", jit=False,
     clip/model.py: pre-projection encode_image, tuple encode_text) or
     "open_clip" (post-projection, one tensor; methods/PEFT_openclip.py); it
     defaults to "open_clip" for open_clip model names (OPEN_CLIP_MODELS).
+    `config` (a CLIPConfig or a MODEL_CONFIGS name) fixes the architecture of a
+    state-dict file instead of inferring it: shape inference (build_model) cannot
+    see the activation or the vision head width, so an open_clip ViT-H-14 file
+    needs config="ViT-H-14" (exact GELU, 16 heads of 80); every tensor's shape is
+    then checked against that config.
     """
     if surface is None:
         surface = "open_clip" if name in OPEN_CLIP_MODELS else "openai"
@@ -55,12 +61,26 @@ def load(name, device="cuda" if torch.cuda.is_available() else "cpu", jit=False,
         for key in ("input_resolution", "context_length", "vocab_size"):
             sd.pop(key, None)
         cfg = config_from_state_dict(sd)
+        if config is not None:
+            cfg = _checked_config(config, sd, name)
     else:
         raise RuntimeError(f"Model {name} not found; available models = {available_models()}")
     if jit:
         warnings.warn(f"{name}: JIT archives are not supported by miclip; loading as a state dict")
     model = CLIP(cfg, sd, device=device, compute_dtype=compute_dtype, surface=surface).eval()
     return model.state_dict(), model, _transform(cfg.image_resolution)
+
+
+def _checked_config(config, sd, name):
+    from .weights import param_specs
+    cfg = MODEL_CONFIGS[config] if isinstance(config, str) else config
+    for key, shape, _, _ in param_specs(cfg):
+        if key not in sd:
+            raise RuntimeError(f"{name}: missing key {key!r} for the given config")
+        if tuple(sd[key].shape) != tuple(shape):
+            raise RuntimeError(f"{name}: {key} has shape {tuple(sd[key].shape)}, the config "
+                               f"expects {tuple(shape)}")
+    return cfg
 
 
 def tokenize(texts, context_length: int = 77, truncate: bool = False):

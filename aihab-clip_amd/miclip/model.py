@@ -236,6 +236,16 @@ class CLIP(nn.Module):
                                            flops=arr[i].flops, bytes=arr[i].bytes)
                 for i in range(n) if arr[i].launches}
 
+    # open_clip's training hooks (methods/PEFT_openclip.py:197-273 locks towers and
+    # backpropagates through encode_image): outside the inference path built here
+    def lock_image_tower(self, *args, **kwargs):
+        raise NotImplementedError("miclip is an inference path: open_clip's lock_image_tower / "
+                                  "PEFT training (backward through encode_image) is not supported")
+
+    def lock_text_tower(self, *args, **kwargs):
+        raise NotImplementedError("miclip is an inference path: open_clip's lock_text_tower / "
+                                  "PEFT training is not supported")
+
     @torch.no_grad()
     def encode_image(self, image, normalize=False, apply_proj=None, out=None):
         """Pre-projection image features [B, vision_width] (clip/model.py:335-336, 216-235);

@@ -11,12 +11,21 @@ the contract those call sites use, on miclip's open_clip surface
 open_clip's own code.
 
   * create_model_and_transforms -> (model, preprocess_train, preprocess_val):
-    seeded weights of the named shape (no checkpoints offline), or a state-dict
-    file for `pretrained`; both transforms are the eval transform (Resize
+    `pretrained` = a state-dict file (built with the named model's config: exact
+    GELU and 80-wide vision heads for ViT-H-14, shapes checked), or None /
+    "seeded" for seeded weights of the named shape. A pretrained TAG (e.g.
+    "laion2b_s32b_b79k") raises: there are no checkpoints offline, and silently
+    returning random weights would make every downstream accuracy meaningless.
+    Both transforms are the eval transform (Resize
     bicubic + CenterCrop + CLIP normalise, open_clip's default for the OpenAI
     mean/std): the training-time augmentation is outside the encode path.
   * get_tokenizer(name) -> callable(texts, context_length=77): the CLIP BPE
     (open_clip's SimpleTokenizer is the same vocabulary and padding).
+
+Scope: the inference contract only -- model_init, feature caching and eval.
+The PEFT training loop (methods/PEFT_openclip.py:197-273: lock_image_tower /
+lock_text_tower, backward through encode_image) is outside the encode path; the
+model's lock_* methods raise NotImplementedError saying so.
 """
 import os
 
@@ -32,12 +41,23 @@ def list_models():
 def create_model(model_name, pretrained=None, device="cuda", *, compute_dtype="fp16", seed=0,
                  **_unused):
     from . import load
-    src = pretrained if pretrained and os.path.isfile(str(pretrained)) else model_name
-    if src == model_name and model_name not in OPEN_CLIP_MODELS:
+    from .configs import MODEL_CONFIGS
+    if model_name not in OPEN_CLIP_MODELS:
         raise RuntimeError(f"Model config for {model_name} not found; available models "
                            f"{list_models()}.")
+    if pretrained in (None, "", "seeded"):
+        src, config = model_name, None
+    elif os.path.isfile(str(pretrained)):
+        # the named model's architecture, not build_model's shape inference (which
+        # would give QuickGELU and 64-wide heads); load() checks every shape
+        src, config = str(pretrained), MODEL_CONFIGS[model_name]
+    else:
+        raise RuntimeError(
+            f"pretrained={pretrained!r} for {model_name}: no pretrained checkpoints are "
+            f"available offline. Pass a state-dict file path, or pretrained=None / 'seeded' "
+            f"for seeded random weights of the {model_name} shapes.")
     _, model, _ = load(src, device=device, compute_dtype=compute_dtype, seed=seed,
-                       surface="open_clip")
+                       surface="open_clip", config=config)
     return model
 
 

@@ -121,19 +121,75 @@ def generate_state_dict(cfg: CLIPConfig, seed: int = 0, towers=("visual", "text"
     return sd
 
 
-def synthetic_images(batch: int, resolution: int, seed: int = 0, offset: int = 0) -> np.ndarray:
-    """CLIP-normalised synthetic images [B,3,R,R] float32: (U[0,1) - mean_c) / std_c.
+def _halton(i: int, base: int) -> float:
+    f, r = 1.0, 0.0
+    while i > 0:
+        f /= base
+        r += f * (i % base)
+        i //= base
+    return r
+
+
+def _bilinear_grid(g: np.ndarray, R: int) -> np.ndarray:
+    """[C, k, k] control grid -> [C, R, R] by bilinear interpolation at pixel centres."""
+    k = g.shape[1]
+    t = (np.arange(R, dtype=np.float64) + 0.5) / R * (k - 1)
+    i0 = np.clip(np.floor(t).astype(np.int64), 0, k - 2)
+    f = t - i0
+    rows = g[:, i0, :] * (1 - f)[None, :, None] + g[:, i0 + 1, :] * f[None, :, None]
+    return rows[:, :, i0] * (1 - f)[None, None, :] + rows[:, :, i0 + 1] * f[None, None, :]
+
+
+def _structured_image(seed: int, resolution: int, j: int) -> np.ndarray:
+    """Image j of the structured set, pixel values in [0, 1], [3, R, R] float32.
+
+    A low-frequency random field (bilinear over a k x k grid, k in 2..8) plus three
+    oriented gratings, scaled by a per-channel contrast (log-uniform 0.05..0.5) around
+    a per-image base colour taken from a Halton sequence (so the base colours of any
+    16 consecutive images are well spread), plus a little pixel noise, clipped to
+    [0, 1]. Unlike i.i.d. noise, whose CLIP embeddings share ~95 % of their norm,
+    these give image-specific features (inter-image 1-cos >= 1.6e-2 over the
+    fixtures' 16 images on random-init ViT-B/32 and ViT-L/14)."""
+    R = resolution
+    r = _rng(seed, f"structured/{R}/{j}")
+    k = int(r.integers(2, 9))
+    img = _bilinear_grid(r.standard_normal((3, k, k)), R)
+    c = (np.arange(R, dtype=np.float64) + 0.5) / R
+    for _ in range(3):
+        fx, fy = r.uniform(-12, 12, 2)
+        ph = r.uniform(0, 2 * np.pi)
+        amp = r.uniform(0, 0.6, 3)
+        wave = np.sin(2 * np.pi * (fy * c[:, None] + fx * c[None, :]) + ph)
+        img += amp[:, None, None] * wave[None]
+    contrast = np.exp(r.uniform(np.log(0.05), np.log(0.5), 3))
+    base = 0.1 + 0.8 * np.array([_halton(j + 1, 2), _halton(j + 1, 3), _halton(j + 1, 5)])
+    img = base[:, None, None] + contrast[:, None, None] * img
+    img += 0.02 * r.standard_normal(img.shape)
+    return np.clip(img, 0.0, 1.0).astype(np.float32)
+
+
+def synthetic_images(batch: int, resolution: int, seed: int = 0, offset: int = 0,
+                     kind: str = "structured") -> np.ndarray:
+    """CLIP-normalised synthetic images [B,3,R,R] float32: (u - mean_c) / std_c.
 
     Same normalisation as the reference preprocess (clip/clip.py:80). Image i of
     the set is drawn from its own stream, so a shard [offset, offset+batch)
-    equals the same rows of a full batch.
+    equals the same rows of a full batch. kind="structured" (default since r04):
+    per-image low-frequency fields, gratings, base colour and contrast
+    (`_structured_image`), so embeddings of different images differ well beyond
+    the parity tolerance; kind="noise": u ~ U[0,1) per pixel (the r01-r03 fixtures).
     """
     out = np.empty((batch, 3, resolution, resolution), dtype=np.float32)
     mean = np.asarray(CLIP_MEAN, np.float32)[:, None, None]
     std = np.asarray(CLIP_STD, np.float32)[:, None, None]
     for i in range(batch):
-        u = _rng(seed, f"image/{resolution}/{offset + i}").random(
-            (3, resolution, resolution), dtype=np.float32)
+        if kind == "structured":
+            u = _structured_image(seed, resolution, offset + i)
+        elif kind == "noise":
+            u = _rng(seed, f"image/{resolution}/{offset + i}").random(
+                (3, resolution, resolution), dtype=np.float32)
+        else:
+            raise ValueError(f"unknown synthetic image kind {kind!r}")
         out[i] = (u - mean) / std
     return out
 

@@ -37,9 +37,10 @@ enum miclip_status {
   MICLIP_ENOMEM = -4
 };
 
-/* MICLIP_MXFP8: QKV, c_fc and c_proj on OCP MX-fp8 operands (e4m3 + an E8M0 scale
- * per 32 k; weights quantised at load, activations by the producing kernels), the
- * rest as MICLIP_FP16. SURVEY §8f row 4 (C5 fp8 weights); parity unpinned. */
+/* MICLIP_MXFP8: the vision tower's QKV, out-proj, c_fc and c_proj on OCP MX-fp8
+ * operands (e4m3 + an E8M0 scale per 32 k; weights quantised at load, activations
+ * by the producing kernels), the rest -- the whole text tower included -- as
+ * MICLIP_FP16. SURVEY §8f row 4 (C5 fp8 weights); parity unpinned. */
 /* MICLIP_F32: an input element type only (miclip_encode_image_ex images). */
 enum miclip_dtype { MICLIP_FP16 = 0, MICLIP_BF16 = 1, MICLIP_MXFP8 = 2, MICLIP_F32 = 3 };
 /* MICLIP_ACT_GELU_TANH: GELU's tanh form, accepted by the op-level MX-fp8 GEMM

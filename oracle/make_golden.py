@@ -105,6 +105,19 @@ def reference_model(refmodel, sd_np, cfg=None):
     return m.eval().float()
 
 
+def separation(feats, logits):
+    """How far apart the golden images are: the smallest and median 1-cos between
+    the features of two DIFFERENT images, the image-specific share of the norm
+    (|f - mean f| / |f|), and how many distinct golden top-1 classes there are."""
+    f = torch.nn.functional.normalize(feats.double(), dim=-1)
+    n = f.shape[0]
+    off = (1 - f @ f.T)[~torch.eye(n, dtype=torch.bool)]
+    fc = feats.double() - feats.double().mean(0)
+    return dict(inter_1mcos_min=float(off.min()), inter_1mcos_median=float(off.median()),
+                specific_norm_share=float((fc.norm(dim=1) / feats.double().norm(dim=1)).mean()),
+                distinct_top1=int(len(set(logits.argmax(1).tolist()))))
+
+
 def run_config(tag, model_name, n_images, prompts, refs, seed=0):
     refmodel, tok_mod, _, _ = refs
     cfg = MODEL_CONFIGS[model_name]
@@ -154,7 +167,8 @@ def run_config(tag, model_name, n_images, prompts, refs, seed=0):
         tokens=tokens,
         meta=np.frombuffer(json.dumps(dict(
             tag=tag, model=model_name, seed=seed, n_images=n_images,
-            image_crc=checksum(imgs),
+            images="structured", image_crc=checksum(imgs),
+            separation=separation(ref_img, logits),
             weight_crc={n: checksum(sd[n]) for n in (
                 "visual.conv1.weight", "visual.proj", "token_embedding.weight",
                 "visual.transformer.resblocks.0.attn.in_proj_weight")},
@@ -165,6 +179,7 @@ def run_config(tag, model_name, n_images, prompts, refs, seed=0):
     path = os.path.join(OUT, f"{tag}.npz")
     np.savez_compressed(path, **fixture)
     print(f"[golden] {tag}: {path} oracle-vs-reference max|d| = {diffs}")
+    print(f"[golden] {tag}: separation {separation(ref_img, logits)}")
     return diffs
 
 
@@ -179,9 +194,11 @@ def main(only=None):
         hier, _ = templates.gen_prompts(True, True)                    # data/templates.py:236
     c1_prompts = flat[:10]
     all_diffs = {}
-    jobs = [("vitb32", "ViT-B/32", 8, c1_prompts), ("vitb16", "ViT-B/16", 4, flat),
-            ("vitl14", "ViT-L/14", 4, hier), ("vitl14_336", "ViT-L/14@336px", 2, hier),
-            ("vith14", "ViT-H-14", 2, c1_prompts)]
+    # 16 structured images per config (weights.synthetic_images): inter-image
+    # 1-cos >= 10x the 1e-3 parity tolerance, several distinct golden top-1 classes
+    jobs = [("vitb32", "ViT-B/32", 16, c1_prompts), ("vitb16", "ViT-B/16", 16, flat),
+            ("vitl14", "ViT-L/14", 16, hier), ("vitl14_336", "ViT-L/14@336px", 16, hier),
+            ("vith14", "ViT-H-14", 16, hier)]
     for tag, name, n, prompts in jobs:
         if only and tag not in only:
             continue

@@ -156,7 +156,7 @@ def test_cache_openclip_embeddings_layout(golden, tmp_path):
     g = golden("vitb32")
     n = g["meta"]["n_images"]
     imgs = synthetic_images(n, 224, seed=0)
-    labels = np.array([3, 1, 4, 1, 5, 9, 2, 6][:n], dtype=np.int64)
+    labels = np.resize(np.array([3, 1, 4, 1, 5, 9, 2, 6], dtype=np.int64), n)
     meta = {"file_name": [f"img_{i:03d}.jpg" for i in range(n)],
             "plot_word_label": [f"class{l}" for l in labels],
             "l2_label": torch.arange(n) % 3}

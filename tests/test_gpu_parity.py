@@ -6,15 +6,21 @@ weights and inputs go through `miclip.load(...)` -> C ABI -> HIP kernels.
 
 Tolerances (north_star / SURVEY §8c):
   * embeddings: 1 - cos <= 1e-3 per row (image pre-projection features,
-    text x_before and x);
+    text x_before and x), and the same bound on the CENTRED image features
+    (each set minus its mean: only the image-specific part; tests/_parity.py).
+    The goldens hold 16 structured images per config whose features differ by
+    1-cos >= 1.1e-2 between any two images (>= 10x the tolerance, printed);
   * zero-shot top-1: bit-exact on every row whose golden top1-top2 margin
     exceeds the logit error bound measured on that same run (2 x max |dlogit|);
     rows inside the bound are reported, not asserted (random-init CLIP has
-    near-tied logits; SURVEY §7 "Hard parts").
+    near-tied logits; SURVEY §7 "Hard parts"). The golden top-1 column holds
+    >= 3 distinct classes per config, and the number of asserted rows is printed.
 """
 import numpy as np
 import pytest
 import torch
+
+from _parity import one_minus_cos, report, top1_report
 
 pytestmark = pytest.mark.gpu
 
@@ -23,10 +29,7 @@ CONFIGS = [("vitb32", "ViT-B/32"), ("vitb16", "ViT-B/16"), ("vitl14", "ViT-L/14"
            ("vitl14_336", "ViT-L/14@336px"), ("vith14", "ViT-H-14")]
 
 
-def _one_minus_cos(a, b):
-    a = torch.as_tensor(a, dtype=torch.float64)
-    b = torch.as_tensor(b, dtype=torch.float64)
-    return (1 - torch.nn.functional.cosine_similarity(a, b, dim=-1)).numpy()
+_one_minus_cos = one_minus_cos
 
 
 _models = {}
@@ -66,9 +69,7 @@ def test_encode_image_matches_reference(golden, tag, name, dtype):
     m = _model(name, dtype)
     feats = m.encode_image(torch.from_numpy(imgs).cuda()).cpu()
     assert feats.shape == g["image"].shape and feats.dtype == torch.float32
-    d = _one_minus_cos(feats, g["image"])
-    print(f"{tag}/{dtype}: image 1-cos max {d.max():.2e}")
-    assert d.max() <= COS_TOL
+    report(f"{tag}/{dtype}", feats, g["image"], COS_TOL, COS_TOL)
 
 
 def test_fp32_residual_stream_option(golden, monkeypatch):
@@ -118,11 +119,9 @@ def test_zero_shot_top1(golden, tag, name):
     err = np.abs(logits - g["logits"]).max()
     bound = 2 * err
     sure = g["margins"] > bound
-    agree = top[:, 0] == g["topk"][:, 0]
-    print(f"{tag}: max|dlogit| {err:.4f}, margins {np.round(g['margins'], 3)}, "
-          f"top1 agree {agree.sum()}/{len(agree)} (asserted on {sure.sum()})")
+    print(f"{tag}: max|dlogit| {err:.4f}, golden margins {np.round(np.sort(g['margins'])[:4], 3)}..")
     assert err < 1.0
-    assert np.all(agree[sure])
+    top1_report(tag, top[:, 0], g["topk"][:, 0], sure)
 
 
 def test_zero_shot_head_exact_on_reference_features(golden):
@@ -230,11 +229,13 @@ def test_zero_shot_head_vs_torch(B, C, k):
 
 
 # MICLIP_MXFP8: parity unpinned with respect to the
-# reference (no fp8 path there); bounded against the fp32 goldens with fp8
-# tolerances instead of COS_TOL, set a few times above what the block-scaled
-# e4m3 path measures (image 1-cos <= 5.5e-4, text <= 4.9e-3).
+# reference (no fp8 path there). The vision tower runs MX-fp8 GEMMs, bounded
+# against the fp32 goldens with fp8 tolerances a few times above what the
+# block-scaled e4m3 path measures (image 1-cos <= 5.5e-4); the
+# text tower runs fp16 under mxfp8 and meets the north star's 1e-3.
 MX_COS_TOL_IMAGE = 2e-3
-MX_COS_TOL_TEXT = 1e-2
+MX_CENTRED_TOL_IMAGE = 1e-2
+MX_COS_TOL_TEXT = COS_TOL
 
 
 @pytest.mark.parametrize("tag,name", [("vitb32", "ViT-B/32"), ("vith14", "ViT-H-14")])
@@ -245,8 +246,9 @@ def test_mxfp8_encode_within_fp8_tolerance(golden, tag, name):
     imgs = synthetic_images(g["meta"]["n_images"], MODEL_CONFIGS[name].image_resolution, seed=0)
     m = _model(name, "mxfp8")
     feats = m.encode_image(torch.from_numpy(imgs).cuda()).cpu()
-    d = _one_minus_cos(feats, g["image"])
+    report(f"{tag}/mxfp8", feats, g["image"], MX_COS_TOL_IMAGE, MX_CENTRED_TOL_IMAGE)
     xb, xp = m.encode_text(torch.from_numpy(g["tokens"]).long().cuda())
+    db = _one_minus_cos(xb.cpu(), g["text_before"])
     dt = _one_minus_cos(xp.cpu(), g["text_proj"])
-    print(f"{tag}/mxfp8: image 1-cos max {d.max():.2e}, text 1-cos max {dt.max():.2e}")
-    assert d.max() <= MX_COS_TOL_IMAGE and dt.max() <= MX_COS_TOL_TEXT
+    print(f"{tag}/mxfp8: text (fp16 tower) 1-cos max before {db.max():.2e} proj {dt.max():.2e}")
+    assert db.max() <= MX_COS_TOL_TEXT and dt.max() <= MX_COS_TOL_TEXT

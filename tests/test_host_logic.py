@@ -91,3 +91,25 @@ def test_preprocess_shapes():
     x = pre(img)
     assert x.shape == (3, 224, 224) and x.dtype == torch.float32
     assert -2.5 < float(x.min()) and float(x.max()) < 2.7
+
+
+def test_openclip_pretrained_rules():
+    """open_clip.create_model: a checkpoint tag raises (no checkpoints offline, and
+    seeded weights behind a real tag would be silent garbage); an unknown model
+    raises like open_clip; a state-dict file is checked against the NAMED config
+    (ViT-H-14: GELU, 80-wide heads), which build_model's inference cannot see."""
+    from types import SimpleNamespace
+    from miclip import _checked_config
+    from miclip.openclip import create_model
+    with pytest.raises(RuntimeError, match="no pretrained checkpoints"):
+        create_model("ViT-H-14", pretrained="laion2b_s32b_b79k")
+    with pytest.raises(RuntimeError, match="not found"):
+        create_model("ViT-Q-99")
+    cfg = MODEL_CONFIGS["ViT-H-14"]
+    sd = {k: SimpleNamespace(shape=s) for k, s, _, _ in param_specs(cfg)}
+    assert _checked_config("ViT-H-14", sd, "f.pt") is cfg
+    inferred = config_from_state_dict(sd)
+    assert inferred.act == "quick" and cfg.act == "erf"      # why the named config is needed
+    sd["visual.proj"] = SimpleNamespace(shape=(1280, 768))
+    with pytest.raises(RuntimeError, match="visual.proj has shape"):
+        _checked_config("ViT-H-14", sd, "f.pt")

@@ -52,6 +52,27 @@ def test_generator_matches_fixture(golden, states, tag):
     assert checksum(imgs) == g["meta"]["image_crc"]
 
 
+@pytest.mark.parametrize("tag", list(TAGS))
+def test_goldens_are_discriminative(golden, tag):
+    """The fixtures can tell one image from another: >= 16 structured images whose
+    features differ by 1-cos >= 10x the 1e-3 parity tolerance between ANY two of
+    them, an image-specific part of >= 30 % of the norm, and >= 3 distinct golden
+    top-1 classes (the r01-r03 noise images shared ~95 % of their features and one
+    top-1 class)."""
+    g = golden(tag)
+    f = torch.nn.functional.normalize(torch.from_numpy(g["image"]).double(), dim=-1)
+    n = f.shape[0]
+    inter = (1 - f @ f.T)[~torch.eye(n, dtype=torch.bool)]
+    raw = torch.from_numpy(g["image"]).double()
+    share = ((raw - raw.mean(0)).norm(dim=1) / raw.norm(dim=1)).mean().item()
+    distinct = len(set(g["topk"][:, 0].tolist()))
+    print(f"{tag}: {n} images, inter-image 1-cos min {inter.min():.3e}, specific share "
+          f"{share:.2f}, {distinct} distinct top-1")
+    assert g["meta"]["images"] == "structured" and n >= 16
+    assert inter.min().item() >= 10 * 1e-3
+    assert share >= 0.3 and distinct >= 3
+
+
 @pytest.mark.parametrize("tag", ["vitb32", "vitb16", "vitl14", "vith14"])
 def test_oracle_image_bit_exact(golden, states, tag):
     torch.set_num_threads(8)
