@@ -1150,37 +1150,12 @@ __global__ __launch_bounds__(256) void attention_q0_kernel(const T* __restrict__
   }
 }
 
-// MICLIP_ATTN=1 forces the one-head-per-workgroup kernel; 4 the pipelined
-// kernel with the last-chunk split (A/B comparisons).
-int attn_variant() {
-  static int v = [] {
-    const char* e = getenv("MICLIP_ATTN");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
+// Attention kernel variants are chosen by the op-level `variant` argument only
+// (miclip_op_attention, A/B benches); the model path always runs variant 0.
 // s_setprio 1 around each tile's MFMA issue: with 2-3 waves per SIMD the one
 // issuing MFMAs goes first, the others' softmax VALU fills its gaps (ViT-L/14
-// layer: 0.184 -> 0.177 ms, same-box A/B). MICLIP_ATTN_PRIO=0 turns it off.
-int attn_prio() {
-  static int v = [] {
-    const char* e = getenv("MICLIP_ATTN_PRIO");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-
-// MICLIP_ATTN_SPLIT=1 (or variant 4) spreads a 1-2-query last chunk over the
-// other waves. Off by default: at N = 257 it measured level with the 9-wave
-// form (0.183 vs 0.181 ms per ViT-L/14 layer at bs=256, same process).
-bool attn_split() {
-  static bool on = [] {
-    const char* e = getenv("MICLIP_ATTN_SPLIT");
-    return e && atoi(e) != 0;
-  }();
-  return on;
-}
+// layer: 0.184 -> 0.177 ms, same-box A/B).
+constexpr int attn_prio() { return 1; }
 
 // one workgroup per (image, head)
 template <typename T, bool CAUSAL, int DH>
@@ -1217,7 +1192,7 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, 
   const size_t lds = (size_t)Npad * 256;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (variant == 0) {   // MICLIP_ATTN: falls back where the kernel does not apply
-    variant = attn_variant();
+    variant = 0;
     if (variant == 9 && (CAUSAL || N < 257 || N > 259)) variant = 0;
   }
   // two workgroups per CU (default when the queries are 8 full chunks + a small
@@ -1316,7 +1291,7 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, 
     }();
     // split the last chunk's key tiles over the other waves when it holds 1-2 queries
     const int nvalid = N - 32 * (nchunks - 1);
-    const bool split = !CAUSAL && nchunks >= 5 && nvalid <= 2 && (variant == 4 || attn_split());
+    const bool split = !CAUSAL && nchunks >= 5 && nvalid <= 2 && variant == 4;
     const int waves = split ? nchunks - 1 : nchunks;
     const size_t lds_all = 2 * lds + (split ? (size_t)2 * waves * nvalid * 66 * 4 : 0);
     const int per_cu = (int)((160 * 1024) / lds_all) < 1 ? 1 : (int)((160 * 1024) / lds_all);

@@ -113,19 +113,24 @@ struct miclip_model {
   // activations of VisionTransformer / Transformer). Default with fp16 compute;
   // MICLIP_RESID_F32=1 keeps an fp32 stream. bf16 compute always streams fp32.
   int resid16 = 0;
-  // MICLIP_MXFP8: QKV / c_fc / c_proj run on MX-fp8 operands (gemm_mx.hip);
-  // everything else (patch embed, attention, out-proj, stream) as fp16 compute.
+  // MICLIP_MXFP8: the vision tower's QKV / c_fc / c_proj run on MX-fp8 operands
+  // (gemm_mx.hip); everything else (patch embed, attention, the text tower) as
+  // fp16 compute.
   bool mx = false;
   // MX-fp8 models: the VISION tower's attention out-projection on MX-fp8 too (the
   // attention output quantised by quant_mx: 80-wide heads straddle the 32-wide
-  // blocks, so no attention epilogue can); MICLIP_MX_OUT=0 at model creation keeps
-  // it fp16. The text tower keeps fp16 out-proj: there the extra quantisation
-  // raised the text 1-cos from 4.5e-3 to 6.9e-3 (tolerance 1e-2) for a path the
-  // benchmarks do not time; in the vision tower image 1-cos moved 4.90e-4 ->
-  // 4.96e-4 for +1.0 % (C5, same box: profiles/r03/configs/mx_out_ab.txt)
+  // blocks, so no attention epilogue can); MICLIP_OPT_MX_OUT_FP16 keeps it fp16.
+  // Image 1-cos moved 4.90e-4 -> 4.96e-4 for +1.0 % (C5, same box:
+  // profiles/r03/configs/mx_out_ab.txt)
   bool mx_out = false;
+  // MX c_fc epilogue: GELU in its tanh form (default) or exact erf
+  // (MICLIP_OPT_MX_GELU_ERF); see mx_act
+  bool mx_gelu_erf = false;
+  // the last vision block on the CLS rows only (default; MICLIP_OPT_FULL_LAST_BLOCK
+  // clears it, also at run time: miclip_model_set_option)
+  bool cls_last = true;
   // ln_1 / ln_2 folded into the QKV / c_fc GEMMs (fp16 stream models;
-  // MICLIP_LN_FOLD=0 runs the LayerNorm kernels instead); folded weights are
+  // MICLIP_OPT_NO_LN_FOLD runs the LayerNorm kernels instead); folded weights are
   // rebuilt per tower after every weight load
   int lnfold = 0;
   bool folded[2] = {false, false};   // [visual, text]
@@ -178,11 +183,11 @@ namespace {
 // CLS rows only (run_block cls_only)
 enum KClass {
   K_IM2COL, K_GEMM_PATCH, K_LAYERNORM, K_GEMM_QKV, K_ATTENTION, K_GEMM_OUT, K_GEMM_FC,
-  K_GEMM_PROJ, K_HEAD, K_TEXT_EMBED, K_CLS_BLOCK, K_NUM
+  K_GEMM_PROJ, K_HEAD, K_TEXT_EMBED, K_CLS_BLOCK, K_ZERO_SHOT, K_NUM
 };
 const char* const kClassNames[K_NUM] = {"im2col", "gemm_patch", "layernorm", "gemm_qkv",
                                         "attention", "gemm_out", "gemm_fc", "gemm_proj",
-                                        "head", "text_embed", "cls_block"};
+                                        "head", "text_embed", "cls_block", "zero_shot"};
 
 hipEvent_t take_event(miclip_model* m) {
   if (!m->event_pool.empty()) {
@@ -323,7 +328,8 @@ double gemm_bytes(double M, double N, double K, double c_bytes) {
 
 // Build the folded QKV / c_fc weights of one tower (after every weight load).
 int ensure_folded(miclip_model* m, bool visual) {
-  if (!m->lnfold || m->folded[visual ? 0 : 1]) return 0;
+  // an MX model's vision tower quantises the LayerNorm output instead (run_block)
+  if (!m->lnfold || (visual && m->mx) || m->folded[visual ? 0 : 1]) return 0;
   const int W = visual ? m->cfg.vision_width : m->cfg.transformer_width;
   int rc;
   for (Block& b : visual ? m->vblocks : m->tblocks) {
@@ -360,13 +366,9 @@ int ensure_folded(miclip_model* m, bool visual) {
 // c_proj: exact GELU (open_clip's nn.GELU) runs in its tanh form there -- its
 // <= 4.8e-4 deviation (2e-4 relative) is far below the e4m3 step (2^-3), and it issues ~9
 // fewer packed VALU ops per element pair than the erf fit (c_fc 0.68 -> 0.59 ms at
-// M = 65792, profiles/r03/configs/mx_epi.jsonl). MICLIP_MX_GELU_ERF=1 keeps erf.
-int mx_act(int act) {
-  static const bool erf = [] {
-    const char* e = getenv("MICLIP_MX_GELU_ERF");
-    return e && atoi(e) != 0;
-  }();
-  return act == ACT_GELU && !erf ? ACT_GELU_TANH : act;
+// M = 65792, profiles/r03/configs/mx_epi.jsonl). MICLIP_OPT_MX_GELU_ERF keeps erf.
+int mx_act(const miclip_model* m, int act) {
+  return act == ACT_GELU && !m->mx_gelu_erf ? ACT_GELU_TANH : act;
 }
 
 int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, int W, int H,
@@ -417,7 +419,7 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
       MICLIP_HIP(layernorm(dt, w.xc, nullptr, 1, b.ln2_g, b.ln2_b, nullptr, nullptr, items, W, 0,
                            s, r16, w.hq, w.hs));
       MICLIP_HIP(gemm_mx(w.hq, w.hs, b.w_fc, b.s_fc, b.b_fc, w.fq, w.fs, items, 4 * W, W, 5,
-                         mx_act(m->cfg.act), s));
+                         mx_act(m, m->cfg.act), s));
       MICLIP_HIP(gemm_mx(w.fq, w.fs, b.w_proj, b.s_proj, b.b_proj, w.xc, nullptr, items, W, 4 * W,
                          1, ACT_NONE, s));
       return 0;
@@ -466,7 +468,7 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
                 mx ? dM * dW + 4 * dW * dW + 4 * dM * dW : gemm_bytes(dM, 4 * dW, dW, 2));
     if (mx)
       MICLIP_HIP(gemm_mx(w.hq, w.hs, b.w_fc, b.s_fc, b.b_fc, w.fq, w.fs, M, 4 * W, W, 5,
-                         mx_act(m->cfg.act), s));
+                         mx_act(m, m->cfg.act), s));
     else if (fold)
       MICLIP_HIP(gemm_store_ln(dt, w.x, b.wf_fc, b.c_fc, b.cs_fc, w.stats, w.f, M, 4 * W, W,
                                m->cfg.act, s));
@@ -524,13 +526,6 @@ int ensure_aux(miclip_model* m, int n) {
   return 0;
 }
 
-// MICLIP_CLS_LAST=0 runs the vision tower's last block over every row (A/B,
-// tests); default 1: CLS rows only (run_block cls_only)
-bool cls_last_block() {
-  const char* e = getenv("MICLIP_CLS_LAST");   // read per encode call (tests switch it)
-  return !e || atoi(e) != 0;
-}
-
 // encode_image for B images whose workspace window is `w` (clip/model.py:216-235)
 int encode_image_part(miclip_model* m, Workspace w, const void* images, int in_dt, int B,
                       float* out, uint32_t flags, hipStream_t s) {
@@ -563,7 +558,7 @@ int encode_image_part(miclip_model* m, Workspace w, const void* images, int in_d
   }
   // the last block on the CLS rows only (run_block); N beyond attention_q0's
   // range (never for CLIP's towers) runs it whole
-  const bool cls_last = cls_last_block() && N <= 768;
+  const bool cls_last = m->cls_last && N <= 768;
   for (int l = 0; l < c.vision_layers; ++l)
     if ((rc = run_block(m, m->vblocks[l], w, B, N, W, H, dh, 0, s,
                         cls_last && l == c.vision_layers - 1)))
@@ -614,6 +609,11 @@ bool cfg_ok(const miclip_config& c, std::string& why) {
       (c.vision_width % 256 || c.transformer_width % 256))
     return bad("MICLIP_MXFP8 needs widths that are multiples of 256");
   if (c.act != MICLIP_ACT_QUICKGELU && c.act != MICLIP_ACT_GELU) return bad("bad act");
+  if (c.options & ~(MICLIP_OPT_RESID_F32 | MICLIP_OPT_NO_LN_FOLD | MICLIP_OPT_MX_OUT_FP16 |
+                    MICLIP_OPT_MX_GELU_ERF | MICLIP_OPT_FULL_LAST_BLOCK))
+    return bad("unknown options bits");
+  if ((c.options & MICLIP_OPT_RESID_F32) && c.compute_dtype == MICLIP_MXFP8)
+    return bad("MICLIP_OPT_RESID_F32 is not available with MICLIP_MXFP8");
   return true;
 }
 
@@ -637,18 +637,17 @@ int miclip_model_create(const miclip_config* cfg, int device, miclip_model** out
   auto* m = new miclip_model();
   m->cfg = c;
   m->device = device;
+  const uint32_t o = c.options;
   m->mx = cfg->compute_dtype == MICLIP_MXFP8;
-  {
-    const char* e = getenv("MICLIP_MX_OUT");
-    m->mx_out = m->mx && !(e && atoi(e) == 0);
-  }
+  m->mx_out = m->mx && !(o & MICLIP_OPT_MX_OUT_FP16);
+  m->mx_gelu_erf = (o & MICLIP_OPT_MX_GELU_ERF) != 0;
+  m->cls_last = !(o & MICLIP_OPT_FULL_LAST_BLOCK);
   m->dtype = m->mx ? MICLIP_FP16 : cfg->compute_dtype;   // the fp16 kernels' operand type
-  {
-    const char* e = getenv("MICLIP_RESID_F32");
-    m->resid16 = m->mx || (m->dtype == MICLIP_FP16 && !(e && atoi(e) != 0));
-    const char* f = getenv("MICLIP_LN_FOLD");
-    m->lnfold = !m->mx && m->resid16 && !(f && atoi(f) == 0);
-  }
+  // fp16 stream: every MX model (its text tower's folded path included), fp16
+  // compute unless RESID_F32; LN fold on the fp16 stream unless NO_LN_FOLD (MX
+  // vision blocks quantise the LayerNorm output instead: run_block)
+  m->resid16 = m->mx || (m->dtype == MICLIP_FP16 && !(o & MICLIP_OPT_RESID_F32));
+  m->lnfold = m->resid16 && !(o & MICLIP_OPT_NO_LN_FOLD);
   const int P = cfg->vision_patch_size, Wv = cfg->vision_width, Wt = cfg->transformer_width;
   m->Kp = (3 * P * P + 63) / 64 * 64;
   const int g = cfg->image_resolution / P, N = g * g + 1, E = cfg->embed_dim;
@@ -923,6 +922,10 @@ int miclip_zero_shot(miclip_model* m, const float* feats, int32_t B, int32_t app
     if (int rc = dev_alloc(m, (void**)&m->zs_scratch, sizeof(float) * cap)) return rc;
     m->zs_cap = cap;
   }
+  ProfScope p(m, K_ZERO_SHOT, (hipStream_t)stream,
+              2.0 * B * ((apply_proj ? (double)Din * E : 0.0) + (double)E * C),
+              4.0 * ((double)B * Din + (apply_proj ? (double)Din * E : 0.0) + (double)E * C +
+                     (double)B * C));
   MICLIP_HIP(zero_shot(feats, apply_proj ? m->vproj : nullptr, text_weights, logits,
                        topk, B, Din, E, C, scale, topk ? k : 0, (hipStream_t)stream,
                        apply_proj ? m->zs_scratch : nullptr));
@@ -1032,7 +1035,17 @@ int64_t miclip_model_bytes(const miclip_model* m) { return m ? m->bytes : 0; }
 int miclip_model_flags(const miclip_model* m) {
   if (!m) return 0;
   return (m->resid16 ? MICLIP_MODEL_RESID16 : 0) | (m->lnfold ? MICLIP_MODEL_LNFOLD : 0) |
-         (m->mx ? MICLIP_MODEL_MXFP8 : 0);
+         (m->mx ? MICLIP_MODEL_MXFP8 : 0) | (m->cls_last ? MICLIP_MODEL_CLS_LAST : 0) |
+         (m->mx_out ? MICLIP_MODEL_MX_OUT : 0) |
+         (m->mx && !m->mx_gelu_erf ? MICLIP_MODEL_MX_GELU_TANH : 0);
+}
+
+int miclip_model_set_option(miclip_model* m, uint32_t option, int32_t on) {
+  if (!m) return fail(MICLIP_EINVAL, "null model");
+  if (option != MICLIP_OPT_FULL_LAST_BLOCK)
+    return fail(MICLIP_EINVAL, "only MICLIP_OPT_FULL_LAST_BLOCK can change after create");
+  m->cls_last = !on;
+  return 0;
 }
 
 int miclip_op_gemm(int32_t dtype, const void* A, const void* W, const float* bias, void* C,

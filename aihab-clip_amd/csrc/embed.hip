@@ -4,11 +4,12 @@
 //   class_token  class-embedding row + pos[0] (clip/model.py:220-221)
 //   token_embed  token_embedding(text) + positional_embedding and the EOT index
 //                text.argmax(-1) (clip/model.py:339-341, 350)
-//   rowvec_matmul  x_before @ text_projection (clip/model.py:351), fp32
+//   rowvec_matmul  x_before @ text_projection (clip/model.py:351) and
+//                x @ visual.proj: fp32 on the f32-input MFMA (head_proj_kernel)
 //   zero_shot    x @ visual.proj -> F.normalize -> scale * f @ text_weights -> topk
-//                (methods/ProLIP.py:38-41, 288-293; methods/utils.py:16-21), fp32
-// All of these are small next to the transformer blocks; they are written for
-// coalesced access and one launch each, not for MFMA.
+//                (methods/ProLIP.py:38-41, 288-293; methods/utils.py:16-21), fp32:
+//                head_proj_kernel, then head_logits_kernel (one workgroup per row)
+// All of these are small next to the transformer blocks.
 #include "common.h"
 #include "kernels.h"
 
@@ -101,159 +102,135 @@ __global__ __launch_bounds__(64) void eot_kernel(const int64_t* __restrict__ tok
   if (lane == 0) eot_rows[p] = p * L + bi;
 }
 
-__global__ __launch_bounds__(256) void rowvec_matmul_kernel(const float* __restrict__ in,
-                                                            const float* __restrict__ Wm,
-                                                            float* __restrict__ out, int D,
-                                                            int E) {
-  extern __shared__ float xs[];
-  const int r = blockIdx.y;
-  for (int d = threadIdx.x; d < D; d += blockDim.x) xs[d] = in[(size_t)r * D + d];
-  __syncthreads();
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= E) return;
-  float acc = 0.f;
-  for (int d = 0; d < D; ++d) acc = fmaf(xs[d], Wm[(size_t)d * E + e], acc);
-  out[(size_t)r * E + e] = acc;
-}
-
-// out[b, e] = sum_d x[b, d] * W[d, e] (fp32), ROWS rows x 64 columns per
-// workgroup: each W element read (coalesced, 256 B per wave) feeds ROWS FMAs;
-// the 4 waves split d into quarters and the partials are summed in a fixed
-// order (deterministic). Grid: (ceil(B/ROWS), ceil(E/64)) -- enough workgroups
-// to spread visual.proj over the chip (B=256, E=768: 384 workgroups).
-template <int ROWS>
-__global__ __launch_bounds__(256) void rows_matmul_kernel(const float* __restrict__ x,
-                                                          const float* __restrict__ W,
-                                                          float* __restrict__ out, int B,
-                                                          int Din, int E) {
-  extern __shared__ float sm[];
-  float* xs = sm;                   // [ROWS][Din]
-  float* red = xs + ROWS * Din;     // [4][ROWS][64]
-  const int b0 = blockIdx.x * ROWS, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int nr = B - b0 < ROWS ? B - b0 : ROWS;
-  const int col = blockIdx.y * 64 + lane;
-  for (int i = tid; i < ROWS * Din; i += 256) {
-    const int r = i / Din;
-    xs[i] = r < nr ? x[(size_t)(b0 + r) * Din + (i - r * Din)] : 0.f;
-  }
-  __syncthreads();
-  float acc[ROWS];
+// out[b, e] = sum_d x[b, d] * W[d, e] in fp32 on the f32-input MFMA
+// (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32 accumulation; the
+// projection of methods/ProLIP.py:38-41 / clip/model.py:335 and 352). One
+// workgroup = 16 rows x 16 columns; its 4 waves take d in quarters, each a chain
+// of MFMAs, and the 4 partial tiles are summed in a fixed order through LDS
+// (deterministic, batch-invariant: a row's result does not depend on B).
+// Per 16-k step lane (g = lane >> 4, i = lane & 15) loads x[row i][d + 4g .. +3]
+// as one float4 and W[d + 4g + s][col i] for s = 0..3; MFMA s then multiplies the
+// k = d + 4g + s pairs (the same k permutation on both operands). Grid
+// (ceil(B/16), ceil(E/16)): 768 workgroups at B = 256, E = 768. Din % 64 == 0.
+__global__ __launch_bounds__(256) void head_proj_kernel(const float* __restrict__ x,
+                                                        const float* __restrict__ W,
+                                                        float* __restrict__ out, int B, int Din,
+                                                        int E) {
+  __shared__ f32x4 red[3][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
+  const int b0 = blockIdx.x * 16, c0 = blockIdx.y * 16;
+  const int row = b0 + i < B ? b0 + i : B - 1, col = c0 + i < E ? c0 + i : E - 1;
+  const int q = Din / 4, d0 = w * q;
+  const float* xp = x + (size_t)row * Din + d0 + 4 * g;
+  const float* wp = W + (size_t)(d0 + 4 * g) * E + col;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int d = 0; d < q; d += 64) {
+    float4 a[4];
+    float bv[4][4];
 #pragma unroll
-  for (int r = 0; r < ROWS; ++r) acc[r] = 0.f;
-  const int q = (Din + 3) / 4, d0 = w * q, d1 = d0 + q < Din ? d0 + q : Din;
-  if (col < E) {
-    int d = d0;
-    for (; d + 8 <= d1; d += 8) {
-      float wv[8];
+    for (int u = 0; u < 4; ++u) {
+      a[u] = *(const float4*)(xp + d + 16 * u);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) wv[u] = W[(size_t)(d + u) * E + col];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-#pragma unroll
-        for (int r = 0; r < ROWS; ++r) acc[r] = fmaf(xs[r * Din + d + u], wv[u], acc[r]);
+      for (int s2 = 0; s2 < 4; ++s2) bv[u][s2] = wp[(size_t)(d + 16 * u + s2) * E];
     }
-    for (; d < d1; ++d) {
-      const float wv = W[(size_t)d * E + col];
 #pragma unroll
-      for (int r = 0; r < ROWS; ++r) acc[r] = fmaf(xs[r * Din + d], wv, acc[r]);
+    for (int u = 0; u < 4; ++u) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].x, bv[u][0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].y, bv[u][1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].z, bv[u][2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].w, bv[u][3], acc, 0, 0, 0);
     }
   }
-#pragma unroll
-  for (int r = 0; r < ROWS; ++r) red[(w * ROWS + r) * 64 + lane] = acc[r];
+  if (w > 0) red[w - 1][lane] = acc;
   __syncthreads();
-  for (int i = tid; i < nr * 64; i += 256) {
-    const int r = i >> 6, c = i & 63;
-    if (blockIdx.y * 64 + c < E)
-      out[(size_t)(b0 + r) * E + blockIdx.y * 64 + c] =
-          (red[(0 * ROWS + r) * 64 + c] + red[(1 * ROWS + r) * 64 + c]) +
-          (red[(2 * ROWS + r) * 64 + c] + red[(3 * ROWS + r) * 64 + c]);
+  if (w > 0) return;
+  const f32x4 r1 = red[0][lane], r2 = red[1][lane], r3 = red[2][lane];
+  // C layout: lane holds rows 4g .. 4g+3 of column i
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int r = b0 + 4 * g + j;
+    if (r < B && c0 + i < E)
+      out[(size_t)r * E + c0 + i] = (acc[j] + r1[j]) + (r2[j] + r3[j]);
   }
 }
 
-// ROWS images per workgroup: L2-normalise, logits = scale * f @ tw, top-k. With
-// proj != null the projection runs here too (only used when the caller gives
-// no scratch for rows_matmul_kernel).
-template <int ROWS>
-__global__ __launch_bounds__(256) void zero_shot_kernel(const float* __restrict__ x,
-                                                        const float* __restrict__ proj,
-                                                        const float* __restrict__ tw,
-                                                        float* __restrict__ logits,
-                                                        int32_t* __restrict__ topk, int B,
-                                                        int Din, int E, int C, float scale,
-                                                        int k) {
+// The zero-shot head on projected rows f [B, E] (methods/ProLIP.py:288-291,
+// methods/utils.py:16-21): logits = scale * F.normalize(f) @ tw [E, C], then
+// the top-k classes (largest first, ties -> lower index). One workgroup per row:
+// the 4 waves sum |f|^2 over quarters of e (fixed order), then take the classes
+// in chunks of 64 (lane = class, coalesced rows of tw), each wave a quarter of e,
+// partials summed in a fixed order; wave 0 selects the top-k by k wave-wide
+// arg-max reductions over the logits staged in LDS.
+__global__ __launch_bounds__(256) void head_logits_kernel(const float* __restrict__ f,
+                                                          const float* __restrict__ tw,
+                                                          float* __restrict__ logits,
+                                                          int32_t* __restrict__ topk, int E,
+                                                          int C, float scale, int k) {
   extern __shared__ float sm[];
-  float* xs = sm;                 // [ROWS][Din]
-  float* fs = xs + ROWS * Din;    // [ROWS][E]
-  float* ls = fs + ROWS * E;      // [ROWS][C]
-  float* red = ls + ROWS * C;     // [ROWS][4] partial norms, then [ROWS] inverse norms
-  const int b0 = blockIdx.x * ROWS, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int nr = B - b0 < ROWS ? B - b0 : ROWS;
-  for (int i = tid; i < ROWS * Din; i += 256) {
-    const int r = i / Din;
-    xs[i] = r < nr ? x[(size_t)(b0 + r) * Din + (i - r * Din)] : 0.f;
-  }
-  __syncthreads();
-  float n2[ROWS];
-#pragma unroll
-  for (int r = 0; r < ROWS; ++r) n2[r] = 0.f;
+  float* fs = sm;              // [E] the row, normalised
+  float* part = fs + E;        // [4][64] per-wave partial logits of one class chunk
+  float* ls = part + 256;      // [C] logits
+  __shared__ float nred[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* fr = f + (size_t)blockIdx.x * E;
+  float n2 = 0.f;
   for (int e = tid; e < E; e += 256) {
-    float acc[ROWS];
-#pragma unroll
-    for (int r = 0; r < ROWS; ++r) acc[r] = proj ? 0.f : xs[r * Din + e];
-    if (proj) {
-      for (int d = 0; d < Din; ++d) {
-        const float wv = proj[(size_t)d * E + e];
-#pragma unroll
-        for (int r = 0; r < ROWS; ++r) acc[r] = fmaf(xs[r * Din + d], wv, acc[r]);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < ROWS; ++r) {
-      fs[r * E + e] = acc[r];
-      n2[r] += acc[r] * acc[r];
-    }
+    const float v = fr[e];
+    fs[e] = v;
+    n2 = fmaf(v, v, n2);
   }
-#pragma unroll
-  for (int r = 0; r < ROWS; ++r) {
-    const float v = wave_sum(n2[r]);
-    if (lane == 0) red[r * 4 + w] = v;
-  }
+  n2 = wave_sum(n2);
+  if (lane == 0) nred[w] = n2;
   __syncthreads();
-  if (tid < ROWS) {
-    const float t = red[tid * 4] + red[tid * 4 + 1] + red[tid * 4 + 2] + red[tid * 4 + 3];
-    red[ROWS * 4 + tid] = 1.0f / fmaxf(sqrtf(t), 1e-12f);   // F.normalize eps
-  }
+  const float inv = 1.0f / fmaxf(sqrtf((nred[0] + nred[1]) + (nred[2] + nred[3])), 1e-12f);
+  for (int e = tid; e < E; e += 256) fs[e] *= inv;
   __syncthreads();
-  for (int i = tid; i < nr * C; i += 256) {
-    const int r = i / C, c = i - r * C;
-    const float inv = red[ROWS * 4 + r];
+  const int q = (E + 3) / 4, e0 = w * q, e1 = e0 + q < E ? e0 + q : E;
+  for (int c0 = 0; c0 < C; c0 += 64) {
+    const int c = c0 + lane;
     float acc = 0.f;
-    int e = 0;
-    for (; e + 8 <= E; e += 8) {
-      float tv[8];
+    if (c < C) {
+      const float* tp = tw + c;
+      int e = e0;
+      for (; e + 8 <= e1; e += 8) {
+        float t[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) tv[u] = tw[(size_t)(e + u) * C + c];
+        for (int u = 0; u < 8; ++u) t[u] = tp[(size_t)(e + u) * C];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc = fmaf(fs[r * E + e + u] * inv, tv[u], acc);
-    }
-    for (; e < E; ++e) acc = fmaf(fs[r * E + e] * inv, tw[(size_t)e * C + c], acc);
-    ls[r * C + c] = scale * acc;
-    logits[(size_t)(b0 + r) * C + c] = scale * acc;
-  }
-  __syncthreads();
-  if (topk && tid < nr) {
-    // selection of the k largest, ties -> lower index first (sorted, largest first)
-    float* l = ls + tid * C;
-    for (int j = 0; j < k; ++j) {
-      int bi = -1;
-      float bv = -INFINITY;
-      for (int c = 0; c < C; ++c) {
-        const float v = l[c];
-        if (bi < 0 || v > bv) { bv = v; bi = c; }
+        for (int u = 0; u < 8; ++u) acc = fmaf(fs[e + u], t[u], acc);
       }
-      topk[(size_t)(b0 + tid) * k + j] = bi;
-      l[bi] = -INFINITY;
+      for (; e < e1; ++e) acc = fmaf(fs[e], tp[(size_t)e * C], acc);
     }
+    part[w * 64 + lane] = acc;
+    __syncthreads();
+    if (w == 0 && c < C) {
+      const float v = scale * ((part[lane] + part[64 + lane]) + (part[128 + lane] + part[192 + lane]));
+      ls[c] = v;
+      logits[(size_t)blockIdx.x * C + c] = v;
+    }
+    __syncthreads();
+  }
+  if (!topk || w != 0) return;
+  for (int j = 0; j < k; ++j) {
+    float bv = -INFINITY;
+    int bi = C;
+    for (int c = lane; c < C; c += 64) {
+      const float v = ls[c];
+      if (bi == C || v > bv) { bv = v; bi = c; }   // ascending c: ties keep the lower index
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o);
+      const int oi = __shfl_xor(bi, o);
+      if (oi < C && (bi == C || ov > bv || (ov == bv && oi < bi))) { bv = ov; bi = oi; }
+    }
+    if (lane == 0) {
+      topk[(size_t)blockIdx.x * k + j] = bi;
+      ls[bi] = -INFINITY;
+    }
+    // one wave left: its LDS ops are in order; keep the compiler from moving
+    // the next scan's reads above lane 0's write
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
 }
 
@@ -381,40 +358,26 @@ hipError_t token_embed(const int64_t* tokens, const float* tok_emb, const float*
 
 hipError_t rowvec_matmul(const float* in, const float* Wm, float* out, int R, int D, int E,
                          hipStream_t s) {
-  if (R < 1 || D < 1 || E < 1) return hipErrorInvalidValue;
-  if ((size_t)(8 * D + 4 * 8 * 64) * sizeof(float) <= 64 * 1024) {
-    hipLaunchKernelGGL(rows_matmul_kernel<8>, dim3((R + 7) / 8, (E + 63) / 64), dim3(256),
-                       (size_t)(8 * D + 4 * 8 * 64) * sizeof(float), s, in, Wm, out, R, D, E);
-    return hipGetLastError();
-  }
-  hipLaunchKernelGGL(rowvec_matmul_kernel, dim3((E + 255) / 256, R), dim3(256),
-                     D * sizeof(float), s, in, Wm, out, D, E);
+  if (R < 1 || D < 64 || D % 64 || E < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(head_proj_kernel, dim3((R + 15) / 16, (E + 15) / 16), dim3(256), 0, s, in,
+                     Wm, out, R, D, E);
   return hipGetLastError();
 }
 
 hipError_t zero_shot(const float* x, const float* proj, const float* tw, float* logits,
                      int32_t* topk, int B, int Din, int E, int C, float scale, int k,
                      hipStream_t s, float* scratch) {
-  if (B < 1 || C < 1 || E < 1 || k < 0 || k > C || (!proj && Din != E)) return hipErrorInvalidValue;
-  if (proj && scratch && (size_t)8 * Din * 4 + 4 * 8 * 64 * 4 <= 64 * 1024) {
-    // projection spread over the chip, then the head on the projected rows
-    hipLaunchKernelGGL(rows_matmul_kernel<8>, dim3((B + 7) / 8, (E + 63) / 64), dim3(256),
-                       (size_t)(8 * Din + 4 * 8 * 64) * sizeof(float), s, x, proj, scratch, B,
-                       Din, E);
-    x = scratch;
-    proj = nullptr;
-    Din = E;
-  }
-  const size_t per_row = (size_t)(Din + E + C + 5) * sizeof(float);
-  if (8 * per_row <= 64 * 1024) {
-    hipLaunchKernelGGL(zero_shot_kernel<8>, dim3((B + 7) / 8), dim3(256), 8 * per_row, s, x, proj,
-                       tw, logits, topk, B, Din, E, C, scale, k);
-  } else if (per_row <= 64 * 1024) {
-    hipLaunchKernelGGL(zero_shot_kernel<1>, dim3(B), dim3(256), per_row, s, x, proj, tw, logits,
-                       topk, B, Din, E, C, scale, k);
-  } else {
+  if (B < 1 || C < 1 || E < 1 || k < 0 || k > C || (!proj && Din != E) || (proj && !scratch))
     return hipErrorInvalidValue;
+  const size_t lds = (size_t)(E + 256 + C) * sizeof(float);
+  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  if (proj) {
+    // the projection on the f32 MFMA over the whole chip, then the head per row
+    if (hipError_t e = rowvec_matmul(x, proj, scratch, B, Din, E, s)) return e;
+    x = scratch;
   }
+  hipLaunchKernelGGL(head_logits_kernel, dim3(B), dim3(256), lds, s, x, tw, logits, topk, E, C,
+                     scale, k);
   return hipGetLastError();
 }
 

@@ -2122,37 +2122,12 @@ __global__ __launch_bounds__(256, 2) void gemm_pp_kernel(const T* __restrict__ A
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// MICLIP_GEMM=128 forces the 128x128 kernel (A/B comparisons), 256 forces the
-// 256x256 one wherever the shape allows; default picks by problem size.
-int gemm_variant() {
-  static int v = [] {
-    const char* e = getenv("MICLIP_GEMM");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
-// Transposed-accumulator epilogue of the persistent kernel for EpiStore /
-// EpiStoreLN (MICLIP_GEMM_TRACC, default 1; 0 = the fp32 row staging, A/B)
-bool gemm_tracc() {
-  static bool v = [] {
-    const char* e = getenv("MICLIP_GEMM_TRACC");
-    return e ? atoi(e) != 0 : true;
-  }();
-  return v;
-}
-
-// Tile-row group of the 256x256 kernel's grouped order (MICLIP_GEMM_GROUP,
-// default 4; 1 = plain row-major). A variant >= 1000 carries it in its
-// thousands digit (diagnostic A/B through miclip_op_gemm).
-int gemm_group() {
-  static int g = [] {
-    const char* e = getenv("MICLIP_GEMM_GROUP");
-    const int v = e ? atoi(e) : 4;
-    return v < 1 ? 1 : v;
-  }();
-  return g;
-}
+// Kernel variants and schedule switches are chosen by the op-level `variant`
+// argument only (miclip_op_gemm: A/B benches); the model path runs variant 0,
+// which picks by problem size. The library reads no environment variables.
+// Tile-row group of the 256x256 kernel's grouped order (default 4; a variant >=
+// 1000 carries another in its thousands digit).
+constexpr int gemm_group() { return 4; }
 
 int cu_count() {
   static int ncu = [] {
@@ -2165,38 +2140,19 @@ int cu_count() {
   return ncu;
 }
 
-// MICLIP_GEMM_TAIL=0 disables the tail split (every row in 256x256 tiles);
-// a variant with kGemmNoTail set does the same for one call (A/B benches).
+// kGemmNoTail: every row in 256x256 tiles, no row-tail split (A/B benches).
 constexpr int kGemmNoTail = 1 << 16;
-// kGemmTailFirst / MICLIP_GEMM_TAIL_FIRST=1: tail workgroups interleaved with
-// the first tiles (gemm256_kernel, block roles)
+// kGemmTailFirst: tail workgroups interleaved with the first tiles
+// (gemm256_kernel, block roles)
 constexpr int kGemmTailFirst = 1 << 17;
-// kGemmStagger (8 us) / MICLIP_GEMM_STAGGER=<us>: round stagger, see gemm256_kernel
+// kGemmStagger: 8-us round stagger, see gemm256_kernel
 constexpr int kGemmStagger = 1 << 18;
 // kGemmDiag1 / kGemmDiag2: gemm256s_kernel DIAG 1 / 2 (diagnostic, garbage output)
 constexpr int kGemmDiag1 = 1 << 19;
 constexpr int kGemmDiag2 = 1 << 20;
-int gemm_stagger_us() {
-  static int us = [] {
-    const char* e = getenv("MICLIP_GEMM_STAGGER");
-    return e ? atoi(e) : 0;
-  }();
-  return us;
-}
-bool gemm_tail_first() {
-  static bool on = [] {
-    const char* e = getenv("MICLIP_GEMM_TAIL_FIRST");
-    return e && atoi(e) != 0;
-  }();
-  return on;
-}
-bool gemm_tail_enabled() {
-  static bool on = [] {
-    const char* e = getenv("MICLIP_GEMM_TAIL");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
+// kGemmTrAccOff: the persistent kernel's fp32 row-staging epilogue instead of the
+// transposed-accumulator one for EpiStore / EpiStoreLN (A/B)
+constexpr int kGemmTrAccOff = 1 << 21;
 
 // Split of a 256x256 launch into whole rounds of tiles plus a row tail
 // (gemm_tail_wg). The tile-rows kept in tiles are the largest multiple of
@@ -2240,15 +2196,16 @@ template <typename T, class Epi>
 hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hipStream_t s,
                   int variant = 0) {
   if (!gemm_shape_ok(M, N, K)) return hipErrorInvalidValue;
-  const bool notail = (variant & kGemmNoTail) || !gemm_tail_enabled();
+  const bool notail = variant & kGemmNoTail;
   const bool tail_first = variant & kGemmTailFirst;
   const bool stagger = variant & kGemmStagger;
   const int diag = variant & kGemmDiag1 ? 1 : variant & kGemmDiag2 ? 2 : 0;
-  variant &= ~(kGemmNoTail | kGemmTailFirst | kGemmStagger | kGemmDiag1 | kGemmDiag2);
+  const bool variant_tracc_off = variant & kGemmTrAccOff;
+  variant &= ~(kGemmNoTail | kGemmTailFirst | kGemmStagger | kGemmDiag1 | kGemmDiag2 |
+               kGemmTrAccOff);
   const int gm = variant >= 1000 ? variant / 1000 : gemm_group();
   variant %= 1000;
-  const bool env_variant = variant == 0;   // MICLIP_GEMM: falls back where it does not apply
-  if (variant == 0) variant = gemm_variant();
+  const bool env_variant = false;   // an explicit variant never falls back silently
   if (variant != 0 && variant != 128 && variant != 256 && variant != 257 && variant != 258 &&
       variant != 259 && variant != 260 && variant != 2 && variant != 3 && variant != 300 &&
       !(variant >= 400 && variant < 420))
@@ -2297,7 +2254,7 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
     const int ndp = tp.ntm_dp * (N / 256), ncu = cu_count();
     const int grid = ndp < ncu ? ndp : ncu;
     if constexpr (TrAcc<Epi>::value) {
-      if (!gemm_tracc()) {
+      if (variant_tracc_off) {
         hipLaunchKernelGGL((gemm256s_kernel<T, Epi, false>), dim3(grid), dim3(512), 0, s,
                            (const T*)A, (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs,
                            tp.wide & 1);
@@ -2353,12 +2310,12 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
     // intermittently, so it is gone.)
     if (variant == 0) variant = 258;
     TailPlan tp = notail ? TailPlan{(M + 255) / 256, 0, 0} : plan_tail(M, N);
-    if (tp.wgs && (tail_first || gemm_tail_first())) {
+    if (tp.wgs && tail_first) {
       tp.wgs = (tp.wgs + 7) / 8 * 8;   // interleaved 8 per 16 blocks
       tp.wide |= 2;
     }
     {
-      const int us = stagger ? 8 : gemm_stagger_us();
+      const int us = stagger ? 8 : 0;
       const int tiles = tp.ntm_dp * (N / 256);
       if (us > 0 && tiles >= 2 * cu_count()) tp.wide |= (us < 255 ? us : 255) << 8;
     }
@@ -2386,14 +2343,8 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
 
 }  // namespace
 
-// MICLIP_GEMM_NT=1: non-temporal stores of the GEMM output (A/B diagnostic)
-int gemm_nt() {
-  static int v = [] {
-    const char* e = getenv("MICLIP_GEMM_NT");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
+// non-temporal stores of the GEMM output: measured level (A/B diagnostic), off
+constexpr int gemm_nt() { return 0; }
 
 template <typename T>
 hipError_t gemm_store_t(const void* A, const void* W, const float* bias, void* C, int M, int N,

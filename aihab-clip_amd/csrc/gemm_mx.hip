@@ -575,8 +575,7 @@ hipError_t launch_mx(const void* A, const void* SA, const void* W, const void* S
                      int K, Epi epi, hipStream_t s) {
   if (M < 1 || N % 256 || K % 128 || K < 128) return hipErrorInvalidValue;
   const int grid = (M + 255) / 256 * (N / 256);
-  const char* e = getenv("MICLIP_GEMM_GROUP");
-  const int gm = e ? (atoi(e) < 1 ? 1 : atoi(e)) : 4;
+  const int gm = 4;   // tile-row group (r03 sweep: 4 and 2 tie, 8 -1 %, 16 -2.7 %)
   hipLaunchKernelGGL((gemm256_mx_kernel<Epi>), dim3(grid), dim3(512), 0, s, (const uint8_t*)A,
                      (const uint8_t*)SA, (const uint8_t*)W, (const uint8_t*)SW, M, N, K, epi, gm);
   return hipGetLastError();
@@ -589,7 +588,9 @@ size_t mx_scale_bytes(int rows, int K) { return (size_t)((rows + 255) / 256) * (
 hipError_t quant_mx(int in_f16, const void* in, int R, int K, void* q, void* sc, hipStream_t s) {
   if (R < 1 || K % 256) return hipErrorInvalidValue;
   const int segs = R * (K / 256);
-  if (in_f16 && !getenv("MICLIP_QUANT_MX_W4")) {
+  // in_f16: 0 fp32, 1 fp16 (16-B loads, lane-quad blocks), 2 fp16 through the
+  // older 8-lane-block kernel (op level only: the byte-identity test)
+  if (in_f16 == 1) {
     const size_t chunks = (size_t)R * (K / 8);
     hipLaunchKernelGGL(quant_mx_h8_kernel, dim3((unsigned)((chunks + 511) / 512)), dim3(256), 0, s,
                        (const _Float16*)in, chunks, K, (uint8_t*)q, (uint8_t*)sc);

@@ -29,7 +29,7 @@ def _transform(n_px):
 
 def load(name, device="cuda" if torch.cuda.is_available() else "cpu", jit=False,
          download_root=None, *, seed: int = 0, compute_dtype: str = "fp16", surface=None,
-         config=None):
+         config=None, options=None):
     """Counterpart of clip.load (clip/clip.py:89-137): returns (state_dict, model, preprocess).
 
     `name` is a model name from available_models() -- resolved offline to the
@@ -46,7 +46,9 @@ def load(name, device="cuda" if torch.cuda.is_available() else "cpu", jit=False,
     state-dict file instead of inferring it: shape inference (build_model) cannot
     see the activation or the vision head width, so an open_clip ViT-H-14 file
     needs config="ViT-H-14" (exact GELU, 16 heads of 80); every tensor's shape is
-    then checked against that config.
+    then checked against that config. `options` ({name: bool}, model.OPTIONS)
+    selects a non-default numerics path (e.g. {"resid_f32": True}); the library
+    reads no environment variables.
     """
     if surface is None:
         surface = "open_clip" if name in OPEN_CLIP_MODELS else "openai"
@@ -67,7 +69,8 @@ def load(name, device="cuda" if torch.cuda.is_available() else "cpu", jit=False,
         raise RuntimeError(f"Model {name} not found; available models = {available_models()}")
     if jit:
         warnings.warn(f"{name}: JIT archives are not supported by miclip; loading as a state dict")
-    model = CLIP(cfg, sd, device=device, compute_dtype=compute_dtype, surface=surface).eval()
+    model = CLIP(cfg, sd, device=device, compute_dtype=compute_dtype, surface=surface,
+                 options=options).eval()
     return model.state_dict(), model, _transform(cfg.image_resolution)
 
 

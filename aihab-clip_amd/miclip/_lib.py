@@ -10,7 +10,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MICLIP_LIB", os.path.join(_HERE, "libmiclip.so"))
 
-ABI_VERSION = 6          # include/miclip.h MICLIP_ABI_VERSION
+ABI_VERSION = 7          # include/miclip.h MICLIP_ABI_VERSION
 MICLIP_FP16 = 0
 MICLIP_BF16 = 1
 MICLIP_MXFP8 = 2
@@ -22,6 +22,15 @@ MICLIP_FLAG_APPLY_PROJ = 2
 MICLIP_MODEL_RESID16 = 1
 MICLIP_MODEL_LNFOLD = 2
 MICLIP_MODEL_MXFP8 = 4
+MICLIP_MODEL_CLS_LAST = 8
+MICLIP_MODEL_MX_OUT = 16
+MICLIP_MODEL_MX_GELU_TANH = 32
+# miclip_config.options (include/miclip.h MICLIP_OPT_*)
+MICLIP_OPT_RESID_F32 = 1
+MICLIP_OPT_NO_LN_FOLD = 2
+MICLIP_OPT_MX_OUT_FP16 = 4
+MICLIP_OPT_MX_GELU_ERF = 8
+MICLIP_OPT_FULL_LAST_BLOCK = 16
 
 EXPORTS = (
     "miclip_model_create", "miclip_model_load_weights", "miclip_model_load_weights_device",
@@ -29,7 +38,7 @@ EXPORTS = (
     "miclip_encode_image", "miclip_encode_image_ex", "miclip_encode_text", "miclip_zero_shot",
     "miclip_clock_probe",
     "miclip_model_destroy", "miclip_last_error", "miclip_abi_version",
-    "miclip_model_bytes", "miclip_model_flags", "miclip_set_profiling", "miclip_profile_read", "miclip_set_splits", "miclip_image_splits",
+    "miclip_model_bytes", "miclip_model_flags", "miclip_model_set_option", "miclip_set_profiling", "miclip_profile_read", "miclip_set_splits", "miclip_image_splits",
     "miclip_op_gemm", "miclip_op_ln_stats", "miclip_op_ln_fold", "miclip_op_gemm_ln",
     "miclip_op_layernorm", "miclip_op_attention", "miclip_op_attention_q0", "miclip_preprocess",
     "miclip_row_norms", "miclip_class_centroids", "miclip_proto_scores",
@@ -44,7 +53,8 @@ class MiclipConfig(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in (
         "embed_dim", "image_resolution", "vision_layers", "vision_width", "vision_patch_size",
         "context_length", "vocab_size", "transformer_width", "transformer_heads",
-        "transformer_layers", "compute_dtype", "act", "vision_head_dim")]
+        "transformer_layers", "compute_dtype", "act", "vision_head_dim")] + [
+        ("options", ctypes.c_uint32)]
 
 
 class MiclipTensor(ctypes.Structure):
@@ -95,6 +105,7 @@ def load_library(path: str = None):
         "miclip_abi_version": ([], ctypes.c_int),
         "miclip_model_bytes": ([vp], i64),
         "miclip_model_flags": ([vp], ctypes.c_int),
+        "miclip_model_set_option": ([vp, u32, i32], ctypes.c_int),
         "miclip_set_profiling": ([vp, ctypes.c_int], ctypes.c_int),
         "miclip_set_splits": ([vp, i32], ctypes.c_int),
         "miclip_image_splits": ([vp, i32], ctypes.c_int),

@@ -46,6 +46,31 @@ _DTYPES = {"fp16": (_lib.MICLIP_FP16, torch.float16), "float16": (_lib.MICLIP_FP
            "mxfp8": (_lib.MICLIP_MXFP8, torch.float16)}
 
 
+# miclip.load(..., options={...}) / CLIP(..., options=...): the numerics paths of
+# include/miclip.h MICLIP_OPT_* (defaults = the benched path). The library reads
+# no environment variables; every choice that changes results is named here.
+OPTIONS = {
+    "resid_f32": (_lib.MICLIP_OPT_RESID_F32, False),        # fp32 residual stream (fp16 compute)
+    "ln_fold": (_lib.MICLIP_OPT_NO_LN_FOLD, True),          # ln_1/ln_2 folded into QKV/c_fc
+    "mx_out": (_lib.MICLIP_OPT_MX_OUT_FP16, True),          # mxfp8: MX vision out-projection
+    "mx_gelu_tanh": (_lib.MICLIP_OPT_MX_GELU_ERF, True),    # mxfp8: tanh-form GELU in MX c_fc
+    "cls_last": (_lib.MICLIP_OPT_FULL_LAST_BLOCK, True),    # last vision block on CLS rows
+}
+
+
+def option_bits(options=None):
+    """{name: bool} -> MICLIP_OPT_* bits (a bit is set where the value departs
+    from the default: the default of every option is 0 bits)."""
+    bits = 0
+    for k, v in (options or {}).items():
+        if k not in OPTIONS:
+            raise ValueError(f"unknown miclip option {k!r}; known: {sorted(OPTIONS)}")
+        bit, default = OPTIONS[k]
+        if bool(v) != default:
+            bits |= bit
+    return bits
+
+
 class _Node(nn.Module):
     """Container mirroring one level of the reference module tree."""
 
@@ -53,7 +78,7 @@ class _Node(nn.Module):
 class _Handle:
     """Owns one miclip_model* (device-bound)."""
 
-    def __init__(self, cfg: CLIPConfig, compute_dtype: int, device_index: int):
+    def __init__(self, cfg: CLIPConfig, compute_dtype: int, device_index: int, options: int = 0):
         self.lib = _lib.load_library()
         c = _lib.MiclipConfig(
             embed_dim=cfg.embed_dim, image_resolution=cfg.image_resolution,
@@ -63,7 +88,7 @@ class _Handle:
             transformer_heads=cfg.transformer_heads, transformer_layers=cfg.transformer_layers,
             compute_dtype=compute_dtype,
             act=_lib.MICLIP_ACT_GELU if cfg.act == "erf" else _lib.MICLIP_ACT_QUICKGELU,
-            vision_head_dim=cfg.vision_head_width)
+            vision_head_dim=cfg.vision_head_width, options=options)
         h = ctypes.c_void_p()
         _lib.check(self.lib.miclip_model_create(ctypes.byref(c), device_index, ctypes.byref(h)),
                    "miclip_model_create")
@@ -115,8 +140,9 @@ SURFACES = ("openai", "open_clip")
 
 class CLIP(nn.Module):
     def __init__(self, cfg: CLIPConfig, state_dict, device="cuda", compute_dtype="fp16",
-                 surface="openai"):
+                 surface="openai", options=None):
         super().__init__()
+        self._options = option_bits(options)
         if compute_dtype not in _DTYPES:
             raise ValueError(f"compute_dtype must be one of {sorted(_DTYPES)}")
         if surface not in SURFACES:
@@ -167,7 +193,7 @@ class CLIP(nn.Module):
             return
         if self._handle is not None:
             self._handle.close()
-        h = _Handle(self.config, _DTYPES[self.compute_dtype][0], idx)
+        h = _Handle(self.config, _DTYPES[self.compute_dtype][0], idx, self._options)
         h.load_device(list(self.state_dict().items()))
         self._handle = h
 
@@ -214,12 +240,22 @@ class CLIP(nn.Module):
         return n
 
     def numerics(self):
-        """The handle's numerics path: dict(resid16, lnfold, mxfp8) (miclip_model_flags)."""
+        """The handle's numerics path (miclip_model_flags): every option that changes
+        what the kernels compute, as the handle runs it."""
         h = self._require()
         f = h.lib.miclip_model_flags(h.ptr)
         return dict(resid16=bool(f & _lib.MICLIP_MODEL_RESID16),
                     lnfold=bool(f & _lib.MICLIP_MODEL_LNFOLD),
-                    mxfp8=bool(f & _lib.MICLIP_MODEL_MXFP8))
+                    mxfp8=bool(f & _lib.MICLIP_MODEL_MXFP8),
+                    cls_last=bool(f & _lib.MICLIP_MODEL_CLS_LAST),
+                    mx_out=bool(f & _lib.MICLIP_MODEL_MX_OUT),
+                    mx_gelu_tanh=bool(f & _lib.MICLIP_MODEL_MX_GELU_TANH))
+
+    def set_cls_last(self, on=True):
+        """Last vision block on the CLS rows only (default) or over every row."""
+        h = self._require()
+        _lib.check(h.lib.miclip_model_set_option(h.ptr, _lib.MICLIP_OPT_FULL_LAST_BLOCK,
+                                                 int(not on)), "miclip_model_set_option")
 
     def set_profiling(self, enable=True):
         h = self._require()

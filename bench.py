@@ -69,7 +69,7 @@ def parse(argv=None):
     ap.add_argument("--splits", type=int, default=2, help="encode_image batch split over streams")
     ap.add_argument("--ab-splits", action="store_true", help="also time splits=1 vs 2 (diagnostic)")
     ap.add_argument("--ab-fold", action="store_true",
-                    help="also time a second model with MICLIP_LN_FOLD=0 in this process (diagnostic)")
+                    help="also time a second model with options ln_fold=False in this process (diagnostic)")
     return ap.parse_args(argv)
 
 
@@ -167,10 +167,11 @@ def attach_traffic(model_name, dtype, epi, M):
 
 # --------------------------------------------------------------------- rank --
 
-def _load_miclip(name, dev, dtype):
+def _load_miclip(name, dev, dtype, options=None):
     import miclip
     # OpenAI surface for every model (pre-projection encode, projection in the head)
-    _, model, _ = miclip.load(name, device=dev, compute_dtype=dtype, surface="openai")
+    _, model, _ = miclip.load(name, device=dev, compute_dtype=dtype, surface="openai",
+                              options=options)
     return model
 
 
@@ -328,7 +329,7 @@ def run(args, backend="nccl", load_model=None):
     value = n_global * args.steps / dt
     clock_ghz, clock_xcd = clock.ghz() if clock is not None else (None, {})
     gf = algorithmic_gflop_per_image(cfg)
-    cls_last = os.environ.get("MICLIP_CLS_LAST", "1").strip() not in ("0", "")   # capi.hip cls_last_block
+    cls_last = model.numerics()["cls_last"]
     gf_exec = executed_gflop_per_image(cfg, cls_last=cls_last)
 
     ab = None
@@ -343,13 +344,7 @@ def run(args, backend="nccl", load_model=None):
         model.set_splits(args.splits)
     abf = None
     if args.ab_fold:
-        prev = os.environ.get("MICLIP_LN_FOLD")
-        os.environ["MICLIP_LN_FOLD"] = "0"
-        m0 = load_model(args.model, dev, args.dtype)
-        if prev is None:
-            del os.environ["MICLIP_LN_FOLD"]
-        else:
-            os.environ["MICLIP_LN_FOLD"] = prev
+        m0 = load_model(args.model, dev, args.dtype, options={"ln_fold": False})
         m0.reserve(max(hi - lo, 1), args.classes)
         m0.set_splits(args.splits)
         step0 = make_step(m0)

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MICLIP_ABI_VERSION 6
+#define MICLIP_ABI_VERSION 7
 
 enum miclip_status {
   MICLIP_OK = 0,
@@ -69,7 +69,26 @@ typedef struct miclip_config {
   int32_t act;           /* miclip_act: QuickGELU (clip/model.py:160-162) or exact GELU */
   int32_t vision_head_dim; /* 0 or 64: heads = width // 64 (clip/model.py:268); 80: open_clip
                               ViT-H/14 (16 heads of 80 on width 1280) */
+  uint32_t options;        /* MICLIP_OPT_* bits (ABI 7); 0 = the default numerics path */
 } miclip_config;
+
+/* Numerics options of a model handle (miclip_config.options). Every path that
+ * changes what the kernels compute is chosen here, explicitly -- the library
+ * reads no environment variables.
+ * RESID_F32: fp32 residual stream under fp16 compute (default: fp16, the
+ *   reference's GPU model). NO_LN_FOLD: run ln_1 / ln_2 as LayerNorm kernels
+ *   (default: folded into the QKV / c_fc GEMMs on the fp16 stream).
+ * MX_OUT_FP16 (MICLIP_MXFP8): keep the vision out-projection fp16 (default MX-fp8).
+ * MX_GELU_ERF (MICLIP_MXFP8): exact-erf GELU in the MX c_fc epilogue (default: the
+ *   tanh form, <= 4.8e-4 from erf, below the e4m3 step).
+ * FULL_LAST_BLOCK: run the last vision block over every token row (default: the
+ *   CLS rows only after its QKV GEMM, the only rows ln_post reads, clip/model.py:
+ *   226-229); switchable at run time with miclip_model_set_option. */
+#define MICLIP_OPT_RESID_F32 1u
+#define MICLIP_OPT_NO_LN_FOLD 2u
+#define MICLIP_OPT_MX_OUT_FP16 4u
+#define MICLIP_OPT_MX_GELU_ERF 8u
+#define MICLIP_OPT_FULL_LAST_BLOCK 16u
 
 /* One host fp32 tensor of a CLIP state dict, named as in CLIP.state_dict(). */
 typedef struct miclip_tensor {
@@ -205,13 +224,22 @@ const char* miclip_last_error(void);
 int miclip_abi_version(void);
 /* Device-memory bytes currently held by the handle (weights + workspaces). */
 int64_t miclip_model_bytes(const miclip_model* m);
-/* Numerics path the handle runs (fixed at create; env MICLIP_RESID_F32 / MICLIP_LN_FOLD):
+/* Numerics path the handle runs (from miclip_config.options and the dtype):
  * MICLIP_MODEL_RESID16 fp16 residual stream, MICLIP_MODEL_LNFOLD ln_1 / ln_2 folded
- * into the QKV / c_fc GEMMs, MICLIP_MODEL_MXFP8 MX-fp8 GEMM operands. 0 for NULL. */
+ * into the QKV / c_fc GEMMs, MICLIP_MODEL_MXFP8 MX-fp8 GEMM operands (vision tower),
+ * MICLIP_MODEL_CLS_LAST last vision block on the CLS rows, MICLIP_MODEL_MX_OUT MX-fp8
+ * vision out-projection, MICLIP_MODEL_MX_GELU_TANH tanh-form GELU in the MX c_fc
+ * epilogue. 0 for NULL. */
 #define MICLIP_MODEL_RESID16 1
 #define MICLIP_MODEL_LNFOLD 2
 #define MICLIP_MODEL_MXFP8 4
+#define MICLIP_MODEL_CLS_LAST 8
+#define MICLIP_MODEL_MX_OUT 16
+#define MICLIP_MODEL_MX_GELU_TANH 32
 int miclip_model_flags(const miclip_model* m);
+/* Switches a run-time option of a handle (only MICLIP_OPT_FULL_LAST_BLOCK; the
+ * others fix the weight layout at create and return MICLIP_EINVAL). */
+int miclip_model_set_option(miclip_model* m, uint32_t option, int32_t on);
 
 /* ---- diagnostics: per-kernel-class timing with HIP events ---- */
 
@@ -296,7 +324,8 @@ int miclip_op_attention_q0(int32_t dtype, const void* qkv, void* out, int32_t B,
  * An MX-fp8 [rows, K] operand is e4m3 bytes [rows, K] plus a tiled E8M0 scale
  * plane of miclip_mx_scale_bytes(rows, K) bytes (one scale per 32 consecutive k). */
 int64_t miclip_mx_scale_bytes(int32_t rows, int32_t K);
-/* rows [R, K] (fp32, or fp16 if in_f16; K % 256 == 0) -> q [R, K] + scales */
+/* rows [R, K] (in_f16: 0 fp32, 1 fp16, 2 fp16 through the older 8-lane-block
+ * kernel -- byte-identical, kept for that test; K % 256 == 0) -> q [R, K] + scales */
 int miclip_op_quant_mx(const void* in, int32_t in_f16, int32_t R, int32_t K, void* q, void* scales,
                        void* stream);
 /* C = A . W^T on MX-fp8 operands (N % 256 == 0, K % 128 == 0). epi 0: C fp16 =

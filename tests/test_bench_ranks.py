@@ -44,7 +44,8 @@ class StubModel:
         return 1
 
     def numerics(self):
-        return dict(resid16=True, lnfold=True, mxfp8=False)
+        return dict(resid16=True, lnfold=True, mxfp8=False, cls_last=True, mx_out=False,
+                    mx_gelu_tanh=False)
 
     def encode_text(self, toks):
         g = torch.Generator().manual_seed(int(toks.sum()) % 1000)
@@ -62,7 +63,7 @@ class StubModel:
         return logits, logits.topk(k, dim=1).indices
 
 
-def _stub_loader(name, dev, dtype):
+def _stub_loader(name, dev, dtype, options=None):
     return StubModel()
 
 

@@ -52,7 +52,7 @@ def test_nm_shows_c_linkage():
 
 def test_abi_version_and_validation(lib):
     from miclip import _lib
-    assert lib.miclip_abi_version() == _lib.ABI_VERSION == 6
+    assert lib.miclip_abi_version() == _lib.ABI_VERSION == 7
     bad = _lib.MiclipConfig(embed_dim=512, image_resolution=224, vision_layers=12, vision_width=700,
                             vision_patch_size=32, context_length=77, vocab_size=49408,
                             transformer_width=512, transformer_heads=8, transformer_layers=12,
@@ -75,3 +75,11 @@ def test_abi_version_and_validation(lib):
     lib.miclip_model_destroy(None)           # no-op on NULL
     assert lib.miclip_model_bytes(None) == 0
     assert lib.miclip_model_flags(None) == 0
+    assert lib.miclip_model_set_option(None, _lib.MICLIP_OPT_FULL_LAST_BLOCK, 1) == -1
+    # unknown option bits are rejected before any device call
+    bad_opt = _lib.MiclipConfig(embed_dim=512, image_resolution=224, vision_layers=12,
+                                vision_width=768, vision_patch_size=32, context_length=77,
+                                vocab_size=49408, transformer_width=512, transformer_heads=8,
+                                transformer_layers=12, compute_dtype=0, act=1, options=1 << 9)
+    assert lib.miclip_model_create(ctypes.byref(bad_opt), 0, ctypes.byref(h)) == -1
+    assert b"options" in lib.miclip_last_error()

@@ -10,8 +10,8 @@ Op level: each piece against float64/fp32 torch, on LayerNorm parameters wider
 than the random-init goldens (gamma log-uniform over [1e-3, 4] with random signs,
 rows whose |mean| is 30-300x their std) and at the benched GEMM shapes (M = 257 *
 {256, 128} and a ragged tail M), against the same GEMM fed the unfolded LayerNorm
-output (the MICLIP_LN_FOLD=0 path), with the same tolerance as tests/test_gpu_kernels.
-Model level: fold vs MICLIP_LN_FOLD=0 against the goldens, and ViT-L/14 fp16 at the
+output (the options={'ln_fold': False} path), with the same tolerance as tests/test_gpu_kernels.
+Model level: fold vs ln_fold=False against the goldens, and ViT-L/14 fp16 at the
 benched batch of 256 (2-stream split, persistent 256x256 GEMMs with row tails) with
 the golden images placed across the split and the tail.
 """
@@ -191,8 +191,8 @@ def _one_minus_cos(a, b):
     return (1 - torch.nn.functional.cosine_similarity(a, b, dim=-1)).numpy()
 
 
-def test_fold_vs_unfolded_model(golden, monkeypatch):
-    """ViT-L/14 fp16: the default (folded) model and MICLIP_LN_FOLD=0 both meet the
+def test_fold_vs_unfolded_model(golden):
+    """ViT-L/14 fp16: the default (folded) model and options={"ln_fold": False} both meet the
     tolerance against the reference goldens, image and text, and agree closely."""
     import miclip
     from miclip.weights import synthetic_images
@@ -201,8 +201,9 @@ def test_fold_vs_unfolded_model(golden, monkeypatch):
     tok = torch.from_numpy(g["tokens"]).long().cuda()
     res = {}
     for fold in ("1", "0"):
-        monkeypatch.setenv("MICLIP_LN_FOLD", fold)
-        _, m, _ = miclip.load("ViT-L/14", device="cuda", compute_dtype="fp16")
+        _, m, _ = miclip.load("ViT-L/14", device="cuda", compute_dtype="fp16",
+                              options={"ln_fold": fold == "1"})
+        assert m.numerics()["lnfold"] == (fold == "1")
         res[fold] = (m.encode_image(imgs).cpu(), m.encode_text(tok)[1].cpu())
         del m
         torch.cuda.empty_cache()
@@ -211,7 +212,7 @@ def test_fold_vs_unfolded_model(golden, monkeypatch):
         print(f"fold={fold}: image 1-cos {di.max():.2e}, text 1-cos {dt.max():.2e}")
         assert di.max() <= COS_TOL and dt.max() <= COS_TOL
     assert _one_minus_cos(res["1"][0], res["0"][0]).max() <= 1e-4
-    assert not torch.equal(res["1"][0], res["0"][0]), "MICLIP_LN_FOLD did not change the path"
+    assert not torch.equal(res["1"][0], res["0"][0]), "ln_fold did not change the path"
 
 
 def test_benched_config_vitl14_bs256(golden):

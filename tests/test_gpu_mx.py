@@ -181,7 +181,7 @@ def test_layernorm_mx(lib, R, D, in_f16):
 
 def test_quant_mx_f16_full_size_matches_lane8_kernel(lib, monkeypatch):
     """ViT-H/14 bs=256 attention output (65 792 x 1280 fp16): the 16-B-load quantiser
-    (default) is byte-identical to the 8-lane-block kernel (MICLIP_QUANT_MX_W4=1),
+    (default) is byte-identical to the 8-lane-block kernel (op-level in_f16 = 2),
     scales included, at the full size the oracle is too slow for."""
     R, K = 65792, 1280
     g = torch.Generator(device="cuda").manual_seed(7)
@@ -192,15 +192,14 @@ def test_quant_mx_f16_full_size_matches_lane8_kernel(lib, monkeypatch):
     x[R - 1, 70] = -300.0
     xh = x.half()
 
-    def run():
+    def run(kind):
         q = torch.empty(R, K, dtype=torch.uint8, device="cuda")
         s = torch.zeros(int(lib.miclip_mx_scale_bytes(R, K)), dtype=torch.uint8, device="cuda")
-        _check(lib, lib.miclip_op_quant_mx(xh.data_ptr(), 1, R, K, q.data_ptr(), s.data_ptr(), _stream()))
+        _check(lib, lib.miclip_op_quant_mx(xh.data_ptr(), kind, R, K, q.data_ptr(), s.data_ptr(), _stream()))
         torch.cuda.synchronize()
         return q, s
 
-    q8, s8 = run()
-    monkeypatch.setenv("MICLIP_QUANT_MX_W4", "1")
-    q4, s4 = run()
+    q8, s8 = run(1)
+    q4, s4 = run(2)
     assert torch.equal(q8, q4)
     assert torch.equal(s8, s4)

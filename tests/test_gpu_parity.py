@@ -72,19 +72,19 @@ def test_encode_image_matches_reference(golden, tag, name, dtype):
     report(f"{tag}/{dtype}", feats, g["image"], COS_TOL, COS_TOL)
 
 
-def test_fp32_residual_stream_option(golden, monkeypatch):
-    """MICLIP_RESID_F32=1 keeps an fp32 residual stream under fp16 compute (the
-    default streams fp16 like the reference's GPU model); both meet the tolerance."""
+def test_fp32_residual_stream_option(golden):
+    """options={"resid_f32": True} keeps an fp32 residual stream under fp16 compute
+    (the default streams fp16 like the reference's GPU model); both meet the tolerance."""
     import miclip
     from miclip.weights import synthetic_images
     g = golden("vitb16")
     imgs = torch.from_numpy(synthetic_images(g["meta"]["n_images"], 224, seed=0)).cuda()
     _models.clear()
-    monkeypatch.setenv("MICLIP_RESID_F32", "1")
-    _, m32, _ = miclip.load("ViT-B/16", device="cuda", compute_dtype="fp16")
+    _, m32, _ = miclip.load("ViT-B/16", device="cuda", compute_dtype="fp16",
+                            options={"resid_f32": True})
+    assert not m32.numerics()["resid16"]
     f32 = m32.encode_image(imgs).cpu()
     del m32
-    monkeypatch.delenv("MICLIP_RESID_F32")
     f16 = _model("ViT-B/16", "fp16").encode_image(imgs).cpu()
     d32, d16 = _one_minus_cos(f32, g["image"]), _one_minus_cos(f16, g["image"])
     print(f"vitb16: 1-cos fp32 stream {d32.max():.2e}, fp16 stream {d16.max():.2e}")
@@ -155,16 +155,21 @@ def test_batch_invariance_and_shards():
 
 @pytest.mark.parametrize("name,dtype,tol", [("ViT-B/16", "fp16", 2e-5), ("ViT-B/32", "bf16", 2e-4),
                                             ("ViT-L/14", "fp16", 2e-5), ("ViT-H-14", "mxfp8", 1e-3)])
-def test_cls_last_block_matches_full(monkeypatch, name, dtype, tol):
+def test_cls_last_block_matches_full(name, dtype, tol):
     """The last vision block on the CLS rows only (default) against the whole
-    block (MICLIP_CLS_LAST=0): the same features up to the CLS attention's
-    summation order (VALU dot products vs MFMA tiles)."""
+    block (set_cls_last(False), MICLIP_OPT_FULL_LAST_BLOCK): the same features up
+    to the CLS attention's summation order (VALU dot products vs MFMA tiles)."""
     from miclip.weights import synthetic_images
     m = _model(name, dtype)
     imgs = torch.from_numpy(synthetic_images(6, 224, seed=5)).cuda()
     fast = m.encode_image(imgs).float().cpu()
-    monkeypatch.setenv("MICLIP_CLS_LAST", "0")
-    full = m.encode_image(imgs).float().cpu()
+    assert m.numerics()["cls_last"]
+    m.set_cls_last(False)
+    try:
+        assert not m.numerics()["cls_last"]
+        full = m.encode_image(imgs).float().cpu()
+    finally:
+        m.set_cls_last(True)
     d = 1 - torch.nn.functional.cosine_similarity(fast, full, dim=1)
     print(f"{name} {dtype}: 1-cos max {d.max().item():.2e}")
     assert d.max().item() <= tol

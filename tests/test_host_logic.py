@@ -113,3 +113,21 @@ def test_openclip_pretrained_rules():
     sd["visual.proj"] = SimpleNamespace(shape=(1280, 768))
     with pytest.raises(RuntimeError, match="visual.proj has shape"):
         _checked_config("ViT-H-14", sd, "f.pt")
+
+
+def test_numerics_options_are_explicit():
+    """Every results-changing path is a named load() option (MICLIP_OPT_* bits);
+    the HIP library reads no environment variables."""
+    import re
+    from miclip.model import OPTIONS, option_bits
+    from miclip import _lib
+    assert option_bits(None) == 0 and option_bits({"ln_fold": True, "cls_last": True}) == 0
+    assert option_bits({"resid_f32": True}) == _lib.MICLIP_OPT_RESID_F32
+    assert option_bits({"ln_fold": False, "cls_last": False}) == (
+        _lib.MICLIP_OPT_NO_LN_FOLD | _lib.MICLIP_OPT_FULL_LAST_BLOCK)
+    with pytest.raises(ValueError, match="unknown miclip option"):
+        option_bits({"fast": True})
+    csrc = os.path.join(os.path.dirname(miclip.__file__), "..", "csrc")
+    for f in os.listdir(csrc):
+        text = open(os.path.join(csrc, f)).read()
+        assert not re.search(r"\bgetenv\s*\(", text), f"{f} reads the environment"
