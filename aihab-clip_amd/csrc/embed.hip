@@ -157,19 +157,21 @@ __global__ __launch_bounds__(256) void head_proj_kernel(const float* __restrict_
 // The zero-shot head on projected rows f [B, E] (methods/ProLIP.py:288-291,
 // methods/utils.py:16-21): logits = scale * F.normalize(f) @ tw [E, C], then
 // the top-k classes (largest first, ties -> lower index). One workgroup per row:
-// the 4 waves sum |f|^2 over quarters of e (fixed order), then take the classes
-// in chunks of 64 (lane = class, coalesced rows of tw), each wave a quarter of e,
-// partials summed in a fixed order; wave 0 selects the top-k by k wave-wide
-// arg-max reductions over the logits staged in LDS.
+// the 4 waves sum |f|^2 (fixed order); then for each chunk of 16 classes every
+// thread takes rows e = tid, tid + 256, ... of tw (16 contiguous floats each,
+// all loads in flight at once), and each class's 256 partials are summed by a
+// wave reduction and the 4 waves in a fixed order; wave 0 selects the top-k by
+// k wave-wide arg-max reductions over the logits staged in LDS.
 __global__ __launch_bounds__(256) void head_logits_kernel(const float* __restrict__ f,
                                                           const float* __restrict__ tw,
                                                           float* __restrict__ logits,
                                                           int32_t* __restrict__ topk, int E,
                                                           int C, float scale, int k) {
+  constexpr int CC = 16;
   extern __shared__ float sm[];
   float* fs = sm;              // [E] the row, normalised
-  float* part = fs + E;        // [4][64] per-wave partial logits of one class chunk
-  float* ls = part + 256;      // [C] logits
+  float* ls = fs + E;          // [C] logits
+  __shared__ float red[4][CC];
   __shared__ float nred[4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const float* fr = f + (size_t)blockIdx.x * E;
@@ -183,30 +185,27 @@ __global__ __launch_bounds__(256) void head_logits_kernel(const float* __restric
   if (lane == 0) nred[w] = n2;
   __syncthreads();
   const float inv = 1.0f / fmaxf(sqrtf((nred[0] + nred[1]) + (nred[2] + nred[3])), 1e-12f);
-  for (int e = tid; e < E; e += 256) fs[e] *= inv;
-  __syncthreads();
-  const int q = (E + 3) / 4, e0 = w * q, e1 = e0 + q < E ? e0 + q : E;
-  for (int c0 = 0; c0 < C; c0 += 64) {
-    const int c = c0 + lane;
-    float acc = 0.f;
-    if (c < C) {
-      const float* tp = tw + c;
-      int e = e0;
-      for (; e + 8 <= e1; e += 8) {
-        float t[8];
+  for (int c0 = 0; c0 < C; c0 += CC) {
+    const int cc = C - c0 < CC ? C - c0 : CC;
+    float acc[CC];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) t[u] = tp[(size_t)(e + u) * C];
+    for (int c = 0; c < CC; ++c) acc[c] = 0.f;
+    for (int e = tid; e < E; e += 256) {
+      const float fe = fs[e] * inv;
+      const float* tr = tw + (size_t)e * C + c0;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc = fmaf(fs[e + u], t[u], acc);
-      }
-      for (; e < e1; ++e) acc = fmaf(fs[e], tp[(size_t)e * C], acc);
+      for (int c = 0; c < CC; ++c) acc[c] = fmaf(fe, tr[c < cc ? c : cc - 1], acc[c]);
     }
-    part[w * 64 + lane] = acc;
+#pragma unroll
+    for (int c = 0; c < CC; ++c) {
+      const float v = wave_sum(acc[c]);
+      if (lane == 0) red[w][c] = v;
+    }
     __syncthreads();
-    if (w == 0 && c < C) {
-      const float v = scale * ((part[lane] + part[64 + lane]) + (part[128 + lane] + part[192 + lane]));
-      ls[c] = v;
-      logits[(size_t)blockIdx.x * C + c] = v;
+    if (tid < cc) {
+      const float v = scale * ((red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]));
+      ls[c0 + tid] = v;
+      logits[(size_t)blockIdx.x * C + c0 + tid] = v;
     }
     __syncthreads();
   }
@@ -369,7 +368,7 @@ hipError_t zero_shot(const float* x, const float* proj, const float* tw, float* 
                      hipStream_t s, float* scratch) {
   if (B < 1 || C < 1 || E < 1 || k < 0 || k > C || (!proj && Din != E) || (proj && !scratch))
     return hipErrorInvalidValue;
-  const size_t lds = (size_t)(E + 256 + C) * sizeof(float);
+  const size_t lds = (size_t)(E + C) * sizeof(float);
   if (lds > 64 * 1024) return hipErrorInvalidValue;
   if (proj) {
     // the projection on the f32 MFMA over the whole chip, then the head per row

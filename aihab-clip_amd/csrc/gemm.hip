@@ -28,6 +28,7 @@
 
 #include <cstdlib>
 #include <type_traits>
+#include <utility>
 
 // MICLIP_STAMPS_KLOOP (scripts/stamps/stamp_gemm_kloop.hip): the persistent
 // kernel's main-loop vmcnt waits get a stamp segment of their own (6; the
@@ -340,10 +341,13 @@ struct TailShape {
   static constexpr int CPW = RG == 1 ? 16 : 32;                    // columns per wave
 };
 
-template <typename T, class Epi, int RG, int TN>
+// NW: waves of the calling workgroup (8: the 512-thread kernels; 4: gemm4s_kernel,
+// where at RG = 2 every wave takes both row groups of its 32 columns).
+template <typename T, class Epi, int RG, int TN, int NW = 8>
 MICLIP_DEV void gemm_tail_wg(const T* __restrict__ A, const T* __restrict__ W, int M, int N,
                              int K, const Epi& epi, int m_start, int task, char* smem) {
   using S = TailShape<RG, TN>;
+  static_assert(NW == 8 || NW == 4, "tail tasks run on 4 or 8 waves");
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ncg = N / TN, rg = task / ncg;
@@ -351,30 +355,34 @@ MICLIP_DEV void gemm_tail_wg(const T* __restrict__ A, const T* __restrict__ W, i
   if (row0 >= M) return;   // whole workgroup (task is workgroup-uniform)
   const int nk = K / 64;
   // LDS-DMA pieces of 8 rows x 128 B: A pieces 0..NA-1 by waves 0..NA-1,
-  // W pieces wave, wave+8, ... (NB / 8 per wave)
+  // W pieces wave, wave+NW, ... (NB / NW per wave)
   const int lchunk = (lane & 7) ^ (lane >> 3);
   int ar = row0 + wave * 8 + (lane >> 3);
   ar = ar < M ? ar : M - 1;
   const T* asrc = A + (size_t)ar * K + lchunk * 8;
   const T* bsrc = W + (size_t)(col0 + wave * 8 + (lane >> 3)) * K + lchunk * 8;
-  constexpr int BPW = S::NB / 8;
+  constexpr int BPW = S::NB / NW;
   const int per_stage = BPW + (wave < S::NA ? 1 : 0);   // LDS-DMA instructions per stage
   auto stage = [&](int t) {
     char* st = smem + (t % S::TS) * S::STG;
     if (wave < S::NA) glds16(asrc + t * 64, st + wave * 1024);
 #pragma unroll
     for (int i = 0; i < BPW; ++i)
-      glds16(bsrc + (size_t)i * 64 * K + t * 64, st + S::SA + (wave + 8 * i) * 1024);
+      glds16(bsrc + (size_t)i * NW * 8 * K + t * 64, st + S::SA + (wave + NW * i) * 1024);
   };
   const int fr = lane & 15, fk = lane >> 4;
   const int sw0 = ((0 + fk) ^ (fr & 7)) << 4, sw1 = ((4 + fk) ^ (fr & 7)) << 4;
-  const int wrow = RG == 1 ? 0 : wave >> 2;           // this wave's row group
+  // row groups per wave: 2 when 4 waves cover RG = 2
+  constexpr int NRW = (NW == 4 && RG == 2) ? 2 : 1;
+  const int wrow = (RG == 1 || NW == 4) ? 0 : wave >> 2;   // this wave's first row group
   const int wcol = (RG == 1 ? wave : wave & 3) * S::CPW;
   const bool active = RG == 2 || wave < 4;
   constexpr int NJ = S::CPW / 16;
-  f32x4 acc[NJ];
+  f32x4 acc[NRW][NJ];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int rr = 0; rr < NRW; ++rr)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[rr][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int t = 0; t < S::TS - 1 && t < nk; ++t) stage(t);
   for (int t = 0; t < nk; ++t) {
     // retire stage t: the younger loads are stages t+1 .. min(t+TS-2, nk-1)
@@ -385,18 +393,21 @@ MICLIP_DEV void gemm_tail_wg(const T* __restrict__ A, const T* __restrict__ W, i
     if (t + S::TS - 1 < nk) stage(t + S::TS - 1);
     if (active) {
       const char* st = smem + (t % S::TS) * S::STG;
-      const char* sa = st + (wrow * 16 + fr) * 128;
-      const i16x8 a0 = *(const i16x8*)(sa + sw0);
-      const i16x8 a1 = *(const i16x8*)(sa + sw1);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const char* sb = st + S::SA + (wcol + j * 16 + fr) * 128;
-        acc[j] = Mfma<T>::m16(a0, *(const i16x8*)(sb + sw0), acc[j]);
-      }
+      for (int rr = 0; rr < NRW; ++rr) {
+        const char* sa = st + ((wrow + rr) * 16 + fr) * 128;
+        const i16x8 a0 = *(const i16x8*)(sa + sw0);
+        const i16x8 a1 = *(const i16x8*)(sa + sw1);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const char* sb = st + S::SA + (wcol + j * 16 + fr) * 128;
-        acc[j] = Mfma<T>::m16(a1, *(const i16x8*)(sb + sw1), acc[j]);
+        for (int j = 0; j < NJ; ++j) {
+          const char* sb = st + S::SA + (wcol + j * 16 + fr) * 128;
+          acc[rr][j] = Mfma<T>::m16(a0, *(const i16x8*)(sb + sw0), acc[rr][j]);
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const char* sb = st + S::SA + (wcol + j * 16 + fr) * 128;
+          acc[rr][j] = Mfma<T>::m16(a1, *(const i16x8*)(sb + sw1), acc[rr][j]);
+        }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -404,12 +415,15 @@ MICLIP_DEV void gemm_tail_wg(const T* __restrict__ A, const T* __restrict__ W, i
   if (!active) return;
   // same register epilogue as the tiles: quad transpose -> 4 consecutive columns
   const int q = (lane & 15) >> 2, jj = lane & 3;
-  const int row = row0 + wrow * 16 + fk * 4 + jj;
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int col = col0 + wcol + j * 16 + 4 * q;
-    const float4 v = quad_transpose(acc[j], lane);
-    if (row < M) epi.put4(row, col, v, epi.bias4(col));
+  for (int rr = 0; rr < NRW; ++rr) {
+    const int row = row0 + (wrow + rr) * 16 + fk * 4 + jj;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = col0 + wcol + j * 16 + 4 * q;
+      const float4 v = quad_transpose(acc[rr][j], lane);
+      if (row < M) epi.put4(row, col, v, epi.bias4(col));
+    }
   }
 }
 
@@ -1339,6 +1353,342 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
 }
 
 // ---------------------------------------------------------------------------
+// gemm4s: 256x256 tiles, 256 threads = 4 waves (2 x 2), 128 x 128 outputs per
+// wave -- ONE wave per SIMD with the 512-register budget: its 8 x 8 grid of
+// 16x16 fp32 accumulators in the AGPR half (the MFMAs are issued from inline asm
+// on "a" operands, so hipcc never moves an accumulator through VGPRs), plus two
+// sets of 16 fragments in VGPRs (the 32-k step being multiplied and the next).
+// The 8-wave kernel (gemm256s_kernel) alternates a compute segment of 16 MFMAs
+// with a load segment (fragment reads, 2 LDS-DMA pieces, a wait, a barrier)
+// between the two waves of a SIMD, and the load segment often outlasts the
+// partner's MFMAs. Here each wave feeds its own matrix pipe:
+// per 32-k step it issues 64 MFMAs and, between them, the 16 fragment reads of the
+// NEXT step (half the LDS bytes per MFMA of the 128 x 64 layout) and its share of
+// the LDS-DMA, with one counted wait + barrier per 64-k K-tile.
+//   * LDS: two stages of 64 KiB (A 256 rows | W 256 rows, 128-B rows = 64 k) with
+//     the 16-B chunk XOR swizzle chunk ^ (row & 7) on the DMA source and on the
+//     read (conflict-free ds_read_b128, as in gemm256s_kernel), and 2 x 4 KiB of
+//     epilogue operands (bias, column sums, row statistics) by tile parity.
+//   * Pipeline over k-steps (two per K-tile G, stage G & 1): the odd step 2G+1
+//     opens with vmcnt(0) + barrier (K-tile G+1 has landed in every wave's view,
+//     and no wave reads stage G & 1 again), reads K-tile G+1's first fragments
+//     while it multiplies, and issues the first DODD of the 16 DMA pieces of
+//     K-tile G+2 into stage G & 1; the even step 2G+2 issues the rest. A DMA
+//     cursor walks the K-tiles of this workgroup's tiles in order (past the last
+//     one it re-fetches the last K-tile into stages nobody reads again, so the
+//     steps stay branch-free). The DMAs are inline asm (hidden from hipcc's
+//     waitcnt pass), so the counted waits are the only ones.
+//   * Persistent over full 256-row tiles: one workgroup per CU walks tiles
+//     blockIdx.x + k * grid in the XCD-grouped order of gemm256s_kernel, and the
+//     stage pipeline runs straight across tile boundaries (the next tile's
+//     K-tile 0 and first fragments are in flight during this tile's epilogue).
+//     Rows past the last full tile-row are row-tail tasks on the same
+//     workgroups (gemm_tail_wg<NW = 4>).
+//   * Epilogue from registers, no LDS staging (both stages stay busy): the MFMA
+//     operands are swapped (C^T = W . A^T), so a lane holds 4 consecutive columns
+//     of one output row per 16x16 block; val4 / val4ln (the functors' exact
+//     operations) convert in registers, one v_permlane16_swap per dword pairs two
+//     blocks so that every lane holds 8 consecutive columns, and each 16-B store
+//     writes 64 contiguous bytes of 16 rows. Same k order and functors as every
+//     other path: outputs bit-identical to gemm256s_kernel and the tail tasks.
+// ---------------------------------------------------------------------------
+// The 256 accumulators live in a0..a255 by hand: every MFMA is an inline-asm
+// statement naming its accumulator registers literally and clobbering the whole
+// AGPR file, so hipcc never holds a value of its own in an AGPR across one and
+// never sees the accumulators as values (given them as C++ values it copied all
+// 256 out at the K-loop exit and spilled ~130 VGPRs). Audit after every edit:
+// `make asm` and require no compiler v_accvgpr_* / scratch in gemm4s_kernel
+// (tests/test_asm_hazards.py checks it). Accumulator (i, j) of the 8 x 8 grid
+// is a[4(8i+j) .. 4(8i+j)+3]. The asm MFMAs are opaque to hipcc's hazard
+// recognizer: the epilogue opens with 16 wait states before its first read.
+#define MICLIP_AGPR_CLOBBERS \
+  "a0", "a1", "a2", "a3", "a4", "a5", "a6", "a7", "a8", "a9", "a10", "a11", "a12", "a13", "a14", "a15", \
+  "a16", "a17", "a18", "a19", "a20", "a21", "a22", "a23", "a24", "a25", "a26", "a27", "a28", "a29", "a30", "a31", \
+  "a32", "a33", "a34", "a35", "a36", "a37", "a38", "a39", "a40", "a41", "a42", "a43", "a44", "a45", "a46", "a47", \
+  "a48", "a49", "a50", "a51", "a52", "a53", "a54", "a55", "a56", "a57", "a58", "a59", "a60", "a61", "a62", "a63", \
+  "a64", "a65", "a66", "a67", "a68", "a69", "a70", "a71", "a72", "a73", "a74", "a75", "a76", "a77", "a78", "a79", \
+  "a80", "a81", "a82", "a83", "a84", "a85", "a86", "a87", "a88", "a89", "a90", "a91", "a92", "a93", "a94", "a95", \
+  "a96", "a97", "a98", "a99", "a100", "a101", "a102", "a103", "a104", "a105", "a106", "a107", "a108", "a109", "a110", "a111", \
+  "a112", "a113", "a114", "a115", "a116", "a117", "a118", "a119", "a120", "a121", "a122", "a123", "a124", "a125", "a126", "a127", \
+  "a128", "a129", "a130", "a131", "a132", "a133", "a134", "a135", "a136", "a137", "a138", "a139", "a140", "a141", "a142", "a143", \
+  "a144", "a145", "a146", "a147", "a148", "a149", "a150", "a151", "a152", "a153", "a154", "a155", "a156", "a157", "a158", "a159", \
+  "a160", "a161", "a162", "a163", "a164", "a165", "a166", "a167", "a168", "a169", "a170", "a171", "a172", "a173", "a174", "a175", \
+  "a176", "a177", "a178", "a179", "a180", "a181", "a182", "a183", "a184", "a185", "a186", "a187", "a188", "a189", "a190", "a191", \
+  "a192", "a193", "a194", "a195", "a196", "a197", "a198", "a199", "a200", "a201", "a202", "a203", "a204", "a205", "a206", "a207", \
+  "a208", "a209", "a210", "a211", "a212", "a213", "a214", "a215", "a216", "a217", "a218", "a219", "a220", "a221", "a222", "a223", \
+  "a224", "a225", "a226", "a227", "a228", "a229", "a230", "a231", "a232", "a233", "a234", "a235", "a236", "a237", "a238", "a239", \
+  "a240", "a241", "a242", "a243", "a244", "a245", "a246", "a247", "a248", "a249", "a250", "a251", "a252", "a253", "a254", "a255"
+
+template <int N, class F, int... I>
+MICLIP_DEV void static_for_impl(F& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+MICLIP_DEV void static_for(F&& f) {
+  static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
+}
+
+// acc[A] += W-fragment . A-fragment^T (operands swapped: C^T = W . A^T); ZERO: C = 0
+template <typename T, int A, bool ZERO>
+MICLIP_DEV void mfma_acc(const i16x8& w, const i16x8& a) {
+  if constexpr (std::is_same_v<T, _Float16>) {
+    if constexpr (ZERO)
+      asm volatile("v_mfma_f32_16x16x32_f16 a[%c2:%c3], %0, %1, 0"
+                   :: "v"(w), "v"(a), "i"(4 * A), "i"(4 * A + 3) : "memory", MICLIP_AGPR_CLOBBERS);
+    else
+      asm volatile("v_mfma_f32_16x16x32_f16 a[%c2:%c3], %0, %1, a[%c2:%c3]"
+                   :: "v"(w), "v"(a), "i"(4 * A), "i"(4 * A + 3) : "memory", MICLIP_AGPR_CLOBBERS);
+  } else {
+    if constexpr (ZERO)
+      asm volatile("v_mfma_f32_16x16x32_bf16 a[%c2:%c3], %0, %1, 0"
+                   :: "v"(w), "v"(a), "i"(4 * A), "i"(4 * A + 3) : "memory", MICLIP_AGPR_CLOBBERS);
+    else
+      asm volatile("v_mfma_f32_16x16x32_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]"
+                   :: "v"(w), "v"(a), "i"(4 * A), "i"(4 * A + 3) : "memory", MICLIP_AGPR_CLOBBERS);
+  }
+}
+// accumulator A into VGPRs (the epilogue)
+template <int A>
+MICLIP_DEV float4 acc_read() {
+  float x, y, z, w;
+  asm volatile(
+      "v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
+      "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
+      : "=v"(x), "=v"(y), "=v"(z), "=v"(w)
+      : "i"(4 * A), "i"(4 * A + 1), "i"(4 * A + 2), "i"(4 * A + 3));
+  return make_float4(x, y, z, w);
+}
+
+template <typename T, class Epi, int DODD = 8>
+__global__ __launch_bounds__(256, 1) void gemm4s_kernel(const T* __restrict__ A,
+                                                        const T* __restrict__ W, int M, int N,
+                                                        int K, Epi epi, int gm, int ntm_dp,
+                                                        int ntail, int tail_wide) {
+  static_assert(TrAcc<Epi>::value, "gemm4s: transposed-accumulator epilogues only");
+  static_assert(DODD >= 0 && DODD <= 16 && DODD % 2 == 0, "DMA split");
+  constexpr bool LN = IsLN<Epi>::value;
+  constexpr bool RES = PrefetchX<Epi>::value;   // fp16 residual stream: x + t at the store
+  constexpr int STAGE = 65536, WOFF = 32768, OPS = 2 * STAGE;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 8192];
+  const int ntn = N / 256, ndp = ntm_dp * ntn, nk = K / 64;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int fr = lane & 15, fk = lane >> 4;
+  // DMA piece = 8 rows x 128 B; lane -> row lane >> 3, source chunk (lane & 7) ^ (lane >> 3)
+  const int prow = lane >> 3, pch = (lane & 7) ^ prow;
+  // fragment reads: row (block base) + fr, logical 16-B chunk 4h + fk
+  const int aoff0 = (wr * 128 + fr) * 128 + (((0 + fk) ^ (fr & 7)) << 4);
+  const int aoff1 = (wr * 128 + fr) * 128 + (((4 + fk) ^ (fr & 7)) << 4);
+  const int boff0 = WOFF + (wc * 128 + fr) * 128 + (((0 + fk) ^ (fr & 7)) << 4);
+  const int boff1 = WOFF + (wc * 128 + fr) * 128 + (((4 + fk) ^ (fr & 7)) << 4);
+  const size_t pstride = (size_t)8 * K;   // elements between the rows of two pieces
+
+  auto tile_of = [&](int id, int& m0_, int& n0_) {
+    int tm_, tn_;
+    group_tile(xcd_remap(id, ndp), ntm_dp, ntn, gm, tm_, tn_);
+    m0_ = tm_ * 256;
+    n0_ = tn_ * 256;
+  };
+  const int ntiles =
+      ndp > (int)blockIdx.x ? (ndp - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+
+  // DMA cursor: the next K-tile to fetch (tile index f_ti of this workgroup, K-tile
+  // f_kt); fa / fw = this lane's source of A / W piece 0 (wave w issues A pieces
+  // 8w..8w+7 = rows m0 + 64w + 8q + prow, and the W pieces likewise)
+  int f_ti = 0, f_kt = 0;
+  const T* fa_p = A;
+  const T* fw_p = W;
+  auto cursor_tile = [&](int ti) {
+    int m0_, n0_;
+    tile_of((int)blockIdx.x + ti * (int)gridDim.x, m0_, n0_);
+    fa_p = A + (size_t)(m0_ + 64 * wave + prow) * K + pch * 8;
+    fw_p = W + (size_t)(n0_ + 64 * wave + prow) * K + pch * 8;
+  };
+  auto advance = [&]() {
+    if (f_kt + 1 < nk) {
+      ++f_kt;
+      fa_p += 64;
+      fw_p += 64;
+    } else if (f_ti + 1 < ntiles) {
+      ++f_ti;
+      f_kt = 0;
+      cursor_tile(f_ti);
+    }   // past the last K-tile: stay (re-fetch into stages nobody reads again)
+  };
+  auto fetch = [&](int q, int st) {   // piece q (0-7 A, 8-15 W) into stage st
+    const char* dst = smem + st * STAGE + (q < 8 ? 0 : WOFF) + (8 * wave + (q & 7)) * 1024;
+    glds16_hidden((q < 8 ? fa_p : fw_p) + (q & 7) * pstride, dst);
+  };
+  // epilogue operands of tile ti into the parity area: bias (wave 0), column sums
+  // (wave 1), the 256 row statistics (waves 2-3, 2 rows per lane); a null bias is
+  // zero-filled. Full tiles only, so every row is in range.
+  auto ops_dma = [&](int ti) {
+    int m0_, n0_;
+    tile_of((int)blockIdx.x + ti * (int)gridDim.x, m0_, n0_);
+    char* o = smem + OPS + (ti & 1) * 4096;
+    int lo = lane;
+    asm volatile("" : "+v"(lo));
+    if (wave == 0) {
+      if (epi.bias)
+        glds16_hidden(epi.bias + n0_ + lo * 4, o);
+      else
+        ((float4*)o)[lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if constexpr (LN) {
+      if (wave == 1) glds16_hidden(epi.colsum + n0_ + lo * 4, o + 1024);
+      if (wave >= 2)
+        glds16_hidden((const float*)(epi.stats + m0_ + (wave - 2) * 128 + 2 * lo),
+                      o + 2048 + (wave - 2) * 1024);
+    }
+  };
+
+  i16x8 fa[2][8], fb[2][8];
+
+  // epilogue of tile ti from the accumulators (see the header)
+  auto epilogue = [&](int ti) {
+    int m0, n0;
+    tile_of((int)blockIdx.x + ti * (int)gridDim.x, m0, n0);
+    const char* o = smem + OPS + (ti & 1) * 4096;
+    // the last MFMAs' results: 16 states before any accumulator read (asm MFMAs
+    // are opaque to hipcc's hazard recognizer)
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    float4 tb[8], tc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c4 = wc * 32 + 4 * j + fk;   // this lane's column quad of block j
+      tb[j] = ((const float4*)o)[c4];
+      tc[j] = LN ? ((const float4*)(o + 1024))[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    auto* outp = tr_out(epi);
+    const int ld = tr_ld(epi);
+    const int colb = n0 + wc * 128 + 16 * (fk & 1) + 8 * (fk >> 1);   // + 32p
+    static_for<8>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      const int rl = wr * 128 + 16 * i + fr;
+      auto* rowp = outp + (size_t)(m0 + rl) * ld + colb;
+      float2 st = make_float2(0.f, 0.f);
+      if constexpr (LN) st = ((const float2*)(o + 2048))[rl];
+      u32x4 xq[4];
+      if constexpr (RES) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) xq[p] = *(const u32x4*)(rowp + 32 * p);
+      }
+      static_for<4>([&](auto pc) {
+        constexpr int p = decltype(pc)::value;
+        const float4 v0 = acc_read<8 * i + 2 * p>(), v1 = acc_read<8 * i + 2 * p + 1>();
+        i16x4 o0, o1;
+        if constexpr (LN) {
+          o0 = epi.val4ln(v0, tb[2 * p], tc[2 * p], st);
+          o1 = epi.val4ln(v1, tb[2 * p + 1], tc[2 * p + 1], st);
+        } else {
+          o0 = epi.val4(v0, tb[2 * p]);
+          o1 = epi.val4(v1, tb[2 * p + 1]);
+        }
+        const u32x2 x0 = __builtin_bit_cast(u32x2, o0), x1 = __builtin_bit_cast(u32x2, o1);
+        // rows 1 / 3 of block 2p <-> rows 0 / 2 of block 2p+1: lane (fr, fk) then
+        // holds columns 8 (fk >> 1) .. +7 of block 2p + (fk & 1)
+        const auto s0 = __builtin_amdgcn_permlane16_swap(x0[0], x1[0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(x0[1], x1[1], false, false);
+        u32x4 w = {s0[0], s1[0], s0[1], s1[1]};
+        if constexpr (RES) {
+          unsigned t[4] = {w[0], w[1], w[2], w[3]};
+          const unsigned x[4] = {xq[p][0], xq[p][1], xq[p][2], xq[p][3]};
+          Epi::template add_x<4>(t, x);
+          w = (u32x4){t[0], t[1], t[2], t[3]};
+        }
+        *(u32x4*)(rowp + 32 * p) = w;
+      });
+    });
+  };
+
+  if (ntiles > 0) {
+    // prologue: operands of tile 0, K-tiles 0 and 1 whole (K >= 128), then F(0)
+    cursor_tile(0);
+    ops_dma(0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) fetch(q, 0);
+    advance();
+#pragma unroll
+    for (int q = 0; q < 16; ++q) fetch(q, 1);
+    advance();
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    lds_barrier();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      fa[0][i] = *(const i16x8*)(smem + aoff0 + i * 2048);
+      fb[0][i] = *(const i16x8*)(smem + boff0 + i * 2048);
+    }
+
+    int G = 0;   // K-tiles this workgroup has entered (stage = G & 1)
+    for (int ti = 0; ti < ntiles; ++ti) {
+      for (int kt = 0; kt < nk; ++kt, ++G) {
+        const int st = G & 1;
+        // ---- even step 2G: multiply F(2G) (set 0), read F(2G+1) (stage st, half 1),
+        // DMA pieces DODD..15 of K-tile G+1 (G >= 1; K-tile 1 came whole in the prologue)
+        auto even = [&](auto first_c, auto dma_c) {
+          constexpr bool FIRST = decltype(first_c)::value, DMA = decltype(dma_c)::value;
+          const char* base = smem + st * STAGE;
+          static_for<8>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            fa[1][i] = *(const i16x8*)(base + aoff1 + i * 2048);
+            fb[1][i] = *(const i16x8*)(base + boff1 + i * 2048);
+            static_for<8>([&](auto jc) {
+              constexpr int j = decltype(jc)::value;
+              mfma_acc<T, 8 * i + j, FIRST>(fb[0][j], fa[0][i]);
+            });
+            if constexpr (DMA) {
+#pragma unroll
+              for (int q = DODD + 2 * i; q < DODD + 2 * i + 2; ++q)
+                if (q < 16) fetch(q, st ^ 1);
+            }
+          });
+          if constexpr (DMA) advance();
+        };
+        if (kt > 0)
+          even(std::false_type{}, std::true_type{});
+        else if (G > 0)
+          even(std::true_type{}, std::true_type{});
+        else
+          even(std::true_type{}, std::false_type{});
+
+        // ---- odd step 2G+1: K-tile G+1 has landed for every wave; stage st is free
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        if (kt == 0 && ti + 1 < ntiles) ops_dma(ti + 1);
+        {
+          const char* base = smem + (st ^ 1) * STAGE;
+          static_for<8>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            fa[0][i] = *(const i16x8*)(base + aoff0 + i * 2048);
+            fb[0][i] = *(const i16x8*)(base + boff0 + i * 2048);
+            static_for<8>([&](auto jc) {
+              constexpr int j = decltype(jc)::value;
+              mfma_acc<T, 8 * i + j, false>(fb[1][j], fa[1][i]);
+            });
+#pragma unroll
+            for (int q = 2 * i; q < 2 * i + 2; ++q)
+              if (q < DODD) fetch(q, st);
+          });
+        }
+      }
+      // ---- this tile's epilogue; the next tile's K-tile 0 and F(0) are in flight
+      epilogue(ti);
+    }
+  }
+  // nothing may land in LDS unretired past this point
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the row tail on the same workgroups
+  for (int task = blockIdx.x; task < ntail; task += gridDim.x) {
+    lds_barrier();
+    if (tail_wide)
+      gemm_tail_wg<T, Epi, 2, 128, 4>(A, W, M, N, K, epi, ntm_dp * 256, task, smem);
+    else
+      gemm_tail_wg<T, Epi, 1, 64, 4>(A, W, M, N, K, epi, ntm_dp * 256, task, smem);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Persistent form of the staggered 256x256 kernel (SCHED 2): one workgroup per
 // CU walks its tiles (ids blockIdx.x + i*gridDim.x, so every round covers the
 // same XCD-grouped tile range as the one-tile-per-workgroup launch) as ONE
@@ -2208,7 +2558,7 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   const bool env_variant = false;   // an explicit variant never falls back silently
   if (variant != 0 && variant != 128 && variant != 256 && variant != 257 && variant != 258 &&
       variant != 259 && variant != 260 && variant != 2 && variant != 3 && variant != 300 &&
-      !(variant >= 400 && variant < 420))
+      !(variant >= 400 && variant < 420) && variant != 508 && variant != 516)
     return hipErrorInvalidValue;
   if constexpr (TrAcc<Epi>::value && !std::is_same_v<Epi, EpiResidual<float>>) {
     // ping-pong kernel: variant 400 + d = start delay of the second workgroup per
@@ -2240,6 +2590,34 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
       return hipGetLastError();
     }
   }
+  if constexpr (TrAcc<Epi>::value && !IsPatch<Epi>::value &&
+                !std::is_same_v<Epi, EpiResidual<float>>) {
+    // 4-wave persistent kernel (gemm4s_kernel): variant 500 + DODD (DMA pieces of
+    // a K-tile issued in the odd k-step; the rest in the even one)
+    if (variant == 508 || variant == 516) {
+      if (N % 256 || K % 64 || K < 128 || M < 256) return hipErrorInvalidValue;
+      // full 256-row tiles only: plan_tail's whole rounds when it splits, else every
+      // full tile-row, the rest (< 256 rows, or <= 256 after whole rounds) as tail tasks
+      TailPlan tp = plan_tail(M, N);
+      if (tp.ntm_dp * 256 > M || notail) {
+        tp.ntm_dp = M / 256;
+        const int rows = M - tp.ntm_dp * 256;
+        tp.wgs = rows > 0 ? (rows + 15) / 16 * (N / 64) : 0;
+        tp.wide = 0;
+      }
+      const int ndp = tp.ntm_dp * (N / 256), ncu = cu_count();
+      const int grid = ndp < ncu ? (ndp > 0 ? ndp : 1) : ncu;
+      if (variant == 508)
+        hipLaunchKernelGGL((gemm4s_kernel<T, Epi, 8>), dim3(grid), dim3(256), 0, s, (const T*)A,
+                           (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs, tp.wide & 1);
+      else
+        hipLaunchKernelGGL((gemm4s_kernel<T, Epi, 16>), dim3(grid), dim3(256), 0, s,
+                           (const T*)A, (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs,
+                           tp.wide & 1);
+      return hipGetLastError();
+    }
+  }
+  if (variant == 508 || variant == 516) return hipErrorInvalidValue;   // not applicable here
   // default for full-size problems: the persistent staggered kernel (variant
   // 259; same-process A/B vs 258 on the ViT-L/14 shapes: QKV +1 %, out-proj +9 %,
   // c_fc +1 %, c_proj +1 %)

@@ -218,26 +218,30 @@ def test_fold_vs_unfolded_model(golden):
 def test_benched_config_vitl14_bs256(golden):
     """The benched configuration -- ViT-L/14 fp16, 256 images, default 2-stream split
     (M = 32896 rows per GEMM launch), persistent GEMMs with row tails, folded LN --
-    with the 4 golden images at rows 0, 127, 128 and 255 (either side of the split
-    and the last row): each within 1-cos 1e-3 of the reference, and bitwise equal to a
-    4-image encode of the same images (row order and batch invariance)."""
+    with the 16 golden images spread over the batch (rows 0, 127, 128 and 255 among
+    them: either side of the split and the last row): each within 1-cos 1e-3 of the
+    reference, the centred features too, and bitwise equal to a 16-image encode of
+    the same images (row order and batch invariance)."""
     import miclip
     from miclip.weights import synthetic_images
+    from _parity import centred_one_minus_cos
     g = golden("vitl14")
-    gold = synthetic_images(4, 224, seed=0)
+    n = g["meta"]["n_images"]
+    gold = synthetic_images(n, 224, seed=0)
     batch = synthetic_images(256, 224, seed=77)
-    rows = [0, 127, 128, 255]
+    rows = [0, 127, 128, 255] + [r for r in range(3, 255, 16) if r not in (127, 128)][:n - 4]
     batch[rows] = gold
     _, m, _ = miclip.load("ViT-L/14", device="cuda", compute_dtype="fp16")
     m.set_splits(2)
-    assert m.image_splits(256) == 2 and m.image_splits(4) == 1
+    assert m.image_splits(256) == 2 and m.image_splits(n) == 1
     feats = m.encode_image(torch.from_numpy(batch).cuda()).cpu()
     d = _one_minus_cos(feats[rows], g["image"])
-    print(f"bs=256 golden rows 1-cos {d}")
-    assert d.max() <= COS_TOL
+    dc = centred_one_minus_cos(feats[rows], g["image"])
+    print(f"bs=256 golden rows 1-cos max {d.max():.2e}, centred {dc.max():.2e}")
+    assert d.max() <= COS_TOL and dc.max() <= COS_TOL
     small = m.encode_image(torch.from_numpy(gold).cuda()).cpu()
     same = [torch.equal(feats[r], small[i]) for i, r in enumerate(rows)]
-    print(f"bitwise equal to the 4-image encode: {same}; max|d| "
+    print(f"bitwise equal to the {n}-image encode: {sum(same)}/{n}; max|d| "
           f"{(feats[rows] - small).abs().max().item():.3e}")
     assert all(same)
     again = m.encode_image(torch.from_numpy(batch).cuda()).cpu()

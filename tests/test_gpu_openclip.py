@@ -127,7 +127,9 @@ def test_openclip_text_weights_and_head(golden, dtype):
     err = (logits.cpu().numpy() - g["logits"]).__abs__().max()
     sure = g["margins"] > 2 * err
     assert err < 1.0
-    top1_report(f"ViT-H-14 open_clip {dtype}", logits.argmax(1).cpu().numpy(), g["topk"][:, 0], sure)
+    # MX-fp8 logits carry ~1e-1 errors, so fewer golden margins clear 2x of it
+    top1_report(f"ViT-H-14 open_clip {dtype}", logits.argmax(1).cpu().numpy(), g["topk"][:, 0], sure,
+                min_rows=8 if dtype == "fp16" else 3)
     # the same through the HIP head kernel (features already projected)
     l2, top = m.zero_shot(m.encode_image(imgs), tw_g, 100.0, k=1, apply_proj=False)
     assert (l2 - logits).abs().max().item() < 2e-3
