@@ -1459,7 +1459,10 @@ MICLIP_DEV float4 acc_read() {
   return make_float4(x, y, z, w);
 }
 
-template <typename T, class Epi, int DODD = 8>
+// DIAG (diagnostic builds, outputs meaningless): 1 = no LDS-DMA after the
+// prologue (the main loop multiplies stale stages), 2 = the epilogue computes but
+// stores nothing. They price the DMA issue and the epilogue stores.
+template <typename T, class Epi, int DODD = 8, int DIAG = 0>
 __global__ __launch_bounds__(256, 1) void gemm4s_kernel(const T* __restrict__ A,
                                                         const T* __restrict__ W, int M, int N,
                                                         int K, Epi epi, int gm, int ntm_dp,
@@ -1516,7 +1519,11 @@ __global__ __launch_bounds__(256, 1) void gemm4s_kernel(const T* __restrict__ A,
       cursor_tile(f_ti);
     }   // past the last K-tile: stay (re-fetch into stages nobody reads again)
   };
+  bool fetch_on = true;   // DIAG 1: off after the prologue
   auto fetch = [&](int q, int st) {   // piece q (0-7 A, 8-15 W) into stage st
+    if constexpr (DIAG == 1) {
+      if (!fetch_on) return;
+    }
     const char* dst = smem + st * STAGE + (q < 8 ? 0 : WOFF) + (8 * wave + (q & 7)) * 1024;
     glds16_hidden((q < 8 ? fa_p : fw_p) + (q & 7) * pstride, dst);
   };
@@ -1597,7 +1604,10 @@ __global__ __launch_bounds__(256, 1) void gemm4s_kernel(const T* __restrict__ A,
           Epi::template add_x<4>(t, x);
           w = (u32x4){t[0], t[1], t[2], t[3]};
         }
-        *(u32x4*)(rowp + 32 * p) = w;
+        if constexpr (DIAG == 2)
+          asm volatile("" ::"v"(w));
+        else
+          *(u32x4*)(rowp + 32 * p) = w;
       });
     });
   };
@@ -1614,6 +1624,7 @@ __global__ __launch_bounds__(256, 1) void gemm4s_kernel(const T* __restrict__ A,
     advance();
     asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     lds_barrier();
+    fetch_on = DIAG != 1;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       fa[0][i] = *(const i16x8*)(smem + aoff0 + i * 2048);
@@ -2607,6 +2618,22 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
       }
       const int ndp = tp.ntm_dp * (N / 256), ncu = cu_count();
       const int grid = ndp < ncu ? (ndp > 0 ? ndp : 1) : ncu;
+      if constexpr (std::is_same_v<Epi, EpiResidual<_Float16>> ||
+                    std::is_same_v<Epi, EpiStore<_Float16, ACT_QUICKGELU>>) {
+        if (diag == 1 && variant == 508) {
+          hipLaunchKernelGGL((gemm4s_kernel<T, Epi, 8, 1>), dim3(grid), dim3(256), 0, s,
+                             (const T*)A, (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs,
+                             tp.wide & 1);
+          return hipGetLastError();
+        }
+        if (diag == 2 && variant == 508) {
+          hipLaunchKernelGGL((gemm4s_kernel<T, Epi, 8, 2>), dim3(grid), dim3(256), 0, s,
+                             (const T*)A, (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs,
+                             tp.wide & 1);
+          return hipGetLastError();
+        }
+      }
+      if (diag) return hipErrorInvalidValue;
       if (variant == 508)
         hipLaunchKernelGGL((gemm4s_kernel<T, Epi, 8>), dim3(grid), dim3(256), 0, s, (const T*)A,
                            (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs, tp.wide & 1);
