@@ -1462,13 +1462,19 @@ MICLIP_DEV float4 acc_read() {
 // DIAG (diagnostic builds, outputs meaningless): 1 = no LDS-DMA after the
 // prologue (the main loop multiplies stale stages), 2 = the epilogue computes but
 // stores nothing. They price the DMA issue and the epilogue stores.
-template <typename T, class Epi, int DODD = 8, int DIAG = 0>
+// DODD of a K-tile's 16 DMA pieces go out in the odd step (spread over its 8
+// MFMA rows), the other 16 - DODD in the even step, spread over its first EROWS
+// rows (they must land before the next odd step's wait)
+template <typename T, class Epi, int DODD = 8, int DIAG = 0, int EROWS = 4>
 __global__ __launch_bounds__(256, 1) void gemm4s_kernel(const T* __restrict__ A,
                                                         const T* __restrict__ W, int M, int N,
                                                         int K, Epi epi, int gm, int ntm_dp,
                                                         int ntail, int tail_wide) {
   static_assert(TrAcc<Epi>::value, "gemm4s: transposed-accumulator epilogues only");
-  static_assert(DODD >= 0 && DODD <= 16 && DODD % 2 == 0, "DMA split");
+  static_assert(DODD >= 0 && DODD <= 16 && EROWS >= 1 && EROWS <= 8, "DMA split");
+  constexpr int PE = 16 - DODD;   // pieces in the even step
+  // pieces of row r: [lo(r), lo(r + 1)) of P spread over R rows
+  constexpr auto lo = [](int r, int P, int R) { return r >= R ? P : (r * P + R - 1) / R; };
   constexpr bool LN = IsLN<Epi>::value;
   constexpr bool RES = PrefetchX<Epi>::value;   // fp16 residual stream: x + t at the store
   constexpr int STAGE = 65536, WOFF = 32768, OPS = 2 * STAGE;
@@ -1650,8 +1656,7 @@ __global__ __launch_bounds__(256, 1) void gemm4s_kernel(const T* __restrict__ A,
             });
             if constexpr (DMA) {
 #pragma unroll
-              for (int q = DODD + 2 * i; q < DODD + 2 * i + 2; ++q)
-                if (q < 16) fetch(q, st ^ 1);
+              for (int q = lo(i, PE, EROWS); q < lo(i + 1, PE, EROWS); ++q) fetch(DODD + q, st ^ 1);
             }
           });
           if constexpr (DMA) advance();
@@ -1678,8 +1683,7 @@ __global__ __launch_bounds__(256, 1) void gemm4s_kernel(const T* __restrict__ A,
               mfma_acc<T, 8 * i + j, false>(fb[1][j], fa[1][i]);
             });
 #pragma unroll
-            for (int q = 2 * i; q < 2 * i + 2; ++q)
-              if (q < DODD) fetch(q, st);
+            for (int q = lo(i, DODD, 8); q < lo(i + 1, DODD, 8); ++q) fetch(q, st);
           });
         }
       }
@@ -2569,7 +2573,8 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   const bool env_variant = false;   // an explicit variant never falls back silently
   if (variant != 0 && variant != 128 && variant != 256 && variant != 257 && variant != 258 &&
       variant != 259 && variant != 260 && variant != 2 && variant != 3 && variant != 300 &&
-      !(variant >= 400 && variant < 420) && variant != 508 && variant != 516)
+      !(variant >= 400 && variant < 420) && variant != 508 && variant != 516 &&
+      !(variant >= 530 && variant <= 534))
     return hipErrorInvalidValue;
   if constexpr (TrAcc<Epi>::value && !std::is_same_v<Epi, EpiResidual<float>>) {
     // ping-pong kernel: variant 400 + d = start delay of the second workgroup per
@@ -2605,7 +2610,7 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
                 !std::is_same_v<Epi, EpiResidual<float>>) {
     // 4-wave persistent kernel (gemm4s_kernel): variant 500 + DODD (DMA pieces of
     // a K-tile issued in the odd k-step; the rest in the even one)
-    if (variant == 508 || variant == 516) {
+    if (variant == 508 || variant == 516 || (variant >= 530 && variant <= 534)) {
       if (N % 256 || K % 64 || K < 128 || M < 256) return hipErrorInvalidValue;
       // full 256-row tiles only: plan_tail's whole rounds when it splits, else every
       // full tile-row, the rest (< 256 rows, or <= 256 after whole rounds) as tail tasks
@@ -2634,6 +2639,22 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
         }
       }
       if (diag) return hipErrorInvalidValue;
+      // DMA-spread experiments (fc / proj epilogues only): 530 (8, 8), 531 (8, 6),
+      // 532 (10, 6), 533 (12, 4), 534 (16, -): (DODD, EROWS)
+      if constexpr (std::is_same_v<Epi, EpiResidual<_Float16>> ||
+                    std::is_same_v<Epi, EpiStore<_Float16, ACT_QUICKGELU>>) {
+#define MICLIP_G4(V, D, E)                                                                 \
+  if (variant == V) {                                                                     \
+    hipLaunchKernelGGL((gemm4s_kernel<T, Epi, D, 0, E>), dim3(grid), dim3(256), 0, s,      \
+                       (const T*)A, (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs,     \
+                       tp.wide & 1);                                                      \
+    return hipGetLastError();                                                             \
+  }
+        MICLIP_G4(530, 8, 8) MICLIP_G4(531, 8, 6) MICLIP_G4(532, 10, 6) MICLIP_G4(533, 12, 4)
+        MICLIP_G4(534, 16, 1)
+#undef MICLIP_G4
+      }
+      if (variant >= 530) return hipErrorInvalidValue;
       if (variant == 508)
         hipLaunchKernelGGL((gemm4s_kernel<T, Epi, 8>), dim3(grid), dim3(256), 0, s, (const T*)A,
                            (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs, tp.wide & 1);
@@ -2644,7 +2665,8 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
       return hipGetLastError();
     }
   }
-  if (variant == 508 || variant == 516) return hipErrorInvalidValue;   // not applicable here
+  if (variant == 508 || variant == 516 || (variant >= 530 && variant <= 534))
+    return hipErrorInvalidValue;   // not applicable here
   // default for full-size problems: the persistent staggered kernel (variant
   // 259; same-process A/B vs 258 on the ViT-L/14 shapes: QKV +1 %, out-proj +9 %,
   // c_fc +1 %, c_proj +1 %)

@@ -117,3 +117,23 @@ def test_gemm4s_rejects_unsupported(lib):
     A2 = torch.zeros(300, 256, device="cuda", dtype=torch.float16)
     assert lib.miclip_op_gemm(0, A2.data_ptr(), W.data_ptr(), b.data_ptr(), X.data_ptr(),
                               300, 256, 256, 1, 0, 508, _stream()) != 0
+
+
+@pytest.mark.parametrize("variant", [530, 531, 532, 533, 534])
+@pytest.mark.parametrize("M,N,K,epi,act", [(65792, 4096, 1024, 0, 1), (32896, 1024, 4096, 4, 0),
+                                           (16421, 1024, 1024, 4, 0)])
+def test_gemm4s_dma_spread_variants_bitexact(lib, variant, M, N, K, epi, act):
+    """The DMA-placement experiments change only when pieces are issued."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + variant)
+    A = (torch.randn(M, K, device="cuda", generator=g) * 0.5).half()
+    W = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).half()
+    bias = torch.randn(N, device="cuda", generator=g) * 0.1
+    X0 = (torch.randn(M, N, device="cuda", generator=g) * 2).half() if epi == 4 else None
+    outs = []
+    for v in (BASE, variant):
+        C = X0.clone() if epi == 4 else torch.empty(M, N, device="cuda", dtype=torch.float16)
+        _check(lib, lib.miclip_op_gemm(0, A.data_ptr(), W.data_ptr(), bias.data_ptr(), C.data_ptr(),
+                                       M, N, K, epi, act, v, _stream()))
+        outs.append(C)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
