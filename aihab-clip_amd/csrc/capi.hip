@@ -129,6 +129,11 @@ struct miclip_model {
   // the last vision block on the CLS rows only (default; MICLIP_OPT_FULL_LAST_BLOCK
   // clears it, also at run time: miclip_model_set_option)
   bool cls_last = true;
+  // GEMM kernel variants for the full-batch launches (M >= 16384 rows), set by
+  // miclip_set_gemm_variant for same-process A/B: [0] the folded-LN store GEMMs
+  // (QKV, c_fc), [1] the fp16 residual GEMMs (out-proj, c_proj). 0 = default.
+  // Only variants bit-identical to the default are accepted: results never change.
+  int gemm_variant[2] = {0, 0};
   // ln_1 / ln_2 folded into the QKV / c_fc GEMMs (fp16 stream models;
   // MICLIP_OPT_NO_LN_FOLD runs the LayerNorm kernels instead); folded weights are
   // rebuilt per tower after every weight load
@@ -374,6 +379,8 @@ int mx_act(const miclip_model* m, int act) {
 int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, int W, int H,
               int dh, int causal, hipStream_t s, bool cls_only = false) {
   const int M = items * N, dt = m->dtype, r16 = m->resid16;
+  const int vln = M >= 16384 ? m->gemm_variant[0] : 0;
+  const int vres = M >= 16384 ? m->gemm_variant[1] : 0;
   const double dM = M, dW = W, rb = r16 ? 2 : 4;  // residual bytes per element
   const bool mx = b.s_qkv != nullptr;   // MX-fp8 operands for QKV / c_fc / c_proj (vision)
   const bool fold = m->lnfold && b.wf_qkv;
@@ -396,7 +403,7 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
                          ACT_NONE, s));
     else if (fold)
       MICLIP_HIP(gemm_store_ln(dt, w.x, b.wf_qkv, b.c_qkv, b.cs_qkv, w.stats, w.qkv, M, 3 * W, W,
-                               ACT_NONE, s));
+                               ACT_NONE, s, vln));
     else
       MICLIP_HIP(gemm_store(dt, w.h, b.w_qkv, b.b_qkv, w.qkv, M, 3 * W, W, ACT_NONE, s));
   }
@@ -448,7 +455,7 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
       MICLIP_HIP(gemm_mx(w.hq, w.hs, b.w_out, b.s_out, b.b_out, w.x, nullptr, M, W, W, 1,
                          ACT_NONE, s));
     } else {
-      MICLIP_HIP(gemm_residual(dt, w.o, b.w_out, b.b_out, w.x, M, W, W, s, 0, r16));
+      MICLIP_HIP(gemm_residual(dt, w.o, b.w_out, b.b_out, w.x, M, W, W, s, r16 ? vres : 0, r16));
     }
   }
   if (fold) {
@@ -471,7 +478,7 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
                          mx_act(m, m->cfg.act), s));
     else if (fold)
       MICLIP_HIP(gemm_store_ln(dt, w.x, b.wf_fc, b.c_fc, b.cs_fc, w.stats, w.f, M, 4 * W, W,
-                               m->cfg.act, s));
+                               m->cfg.act, s, vln));
     else
       MICLIP_HIP(gemm_store(dt, w.h, b.w_fc, b.b_fc, w.f, M, 4 * W, W, m->cfg.act, s));
   }
@@ -483,7 +490,8 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
       MICLIP_HIP(gemm_mx(w.fq, w.fs, b.w_proj, b.s_proj, b.b_proj, w.x, nullptr, M, W, 4 * W, 1,
                          ACT_NONE, s));
     else
-      MICLIP_HIP(gemm_residual(dt, w.f, b.w_proj, b.b_proj, w.x, M, W, 4 * W, s, 0, r16));
+      MICLIP_HIP(gemm_residual(dt, w.f, b.w_proj, b.b_proj, w.x, M, W, 4 * W, s, r16 ? vres : 0,
+                               r16));
   }
   return 0;
 }
@@ -1038,6 +1046,14 @@ int miclip_model_flags(const miclip_model* m) {
          (m->mx ? MICLIP_MODEL_MXFP8 : 0) | (m->cls_last ? MICLIP_MODEL_CLS_LAST : 0) |
          (m->mx_out ? MICLIP_MODEL_MX_OUT : 0) |
          (m->mx && !m->mx_gelu_erf ? MICLIP_MODEL_MX_GELU_TANH : 0);
+}
+
+int miclip_set_gemm_variant(miclip_model* m, int32_t which, int32_t variant) {
+  if (!m || which < 0 || which > 1) return fail(MICLIP_EINVAL, "bad argument to set_gemm_variant");
+  if (variant != 0 && variant != 259 && variant != 508 && variant != 516)
+    return fail(MICLIP_EINVAL, "gemm variant must be 0, 259, 508 or 516 (bit-identical kernels)");
+  m->gemm_variant[which] = variant;
+  return 0;
 }
 
 int miclip_model_set_option(miclip_model* m, uint32_t option, int32_t on) {

@@ -38,7 +38,7 @@ EXPORTS = (
     "miclip_encode_image", "miclip_encode_image_ex", "miclip_encode_text", "miclip_zero_shot",
     "miclip_clock_probe",
     "miclip_model_destroy", "miclip_last_error", "miclip_abi_version",
-    "miclip_model_bytes", "miclip_model_flags", "miclip_model_set_option", "miclip_set_profiling", "miclip_profile_read", "miclip_set_splits", "miclip_image_splits",
+    "miclip_model_bytes", "miclip_model_flags", "miclip_model_set_option", "miclip_set_gemm_variant", "miclip_set_profiling", "miclip_profile_read", "miclip_set_splits", "miclip_image_splits",
     "miclip_op_gemm", "miclip_op_ln_stats", "miclip_op_ln_fold", "miclip_op_gemm_ln",
     "miclip_op_layernorm", "miclip_op_attention", "miclip_op_attention_q0", "miclip_preprocess",
     "miclip_row_norms", "miclip_class_centroids", "miclip_proto_scores",
@@ -106,6 +106,7 @@ def load_library(path: str = None):
         "miclip_model_bytes": ([vp], i64),
         "miclip_model_flags": ([vp], ctypes.c_int),
         "miclip_model_set_option": ([vp, u32, i32], ctypes.c_int),
+        "miclip_set_gemm_variant": ([vp, i32, i32], ctypes.c_int),
         "miclip_set_profiling": ([vp, ctypes.c_int], ctypes.c_int),
         "miclip_set_splits": ([vp, i32], ctypes.c_int),
         "miclip_image_splits": ([vp, i32], ctypes.c_int),

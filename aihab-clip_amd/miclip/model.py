@@ -251,6 +251,13 @@ class CLIP(nn.Module):
                     mx_out=bool(f & _lib.MICLIP_MODEL_MX_OUT),
                     mx_gelu_tanh=bool(f & _lib.MICLIP_MODEL_MX_GELU_TANH))
 
+    def set_gemm_variant(self, which, variant):
+        """Diagnostics: kernel of the full-batch GEMM launches (which 0: QKV / c_fc,
+        1: out-proj / c_proj); bit-identical variants only (miclip_set_gemm_variant)."""
+        h = self._require()
+        _lib.check(h.lib.miclip_set_gemm_variant(h.ptr, int(which), int(variant)),
+                   "miclip_set_gemm_variant")
+
     def set_cls_last(self, on=True):
         """Last vision block on the CLS rows only (default) or over every row."""
         h = self._require()

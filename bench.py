@@ -68,6 +68,9 @@ def parse(argv=None):
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--splits", type=int, default=2, help="encode_image batch split over streams")
     ap.add_argument("--ab-splits", action="store_true", help="also time splits=1 vs 2 (diagnostic)")
+    ap.add_argument("--ab-gemm", default="",
+                    help="diagnostic: also time these GEMM variant pairs 'ln:res,...' (e.g. "
+                         "'0:0,508:0') interleaved in this process (bit-identical kernels)")
     ap.add_argument("--ab-fold", action="store_true",
                     help="also time a second model with options ln_fold=False in this process (diagnostic)")
     return ap.parse_args(argv)
@@ -342,6 +345,20 @@ def run(args, backend="nccl", load_model=None):
             ab.setdefault(f"splits{sp}" + (f"_ran{eff}" if eff != sp else ""), []).append(
                 round(n_global * args.steps / timed(step, args.steps), 1))
         model.set_splits(args.splits)
+    abg = None
+    if args.ab_gemm:
+        abg = {}
+        pairs = [tuple(int(x) for x in p.split(":")) for p in args.ab_gemm.split(",")]
+        for _ in range(3):
+            for vl, vr in pairs:
+                model.set_gemm_variant(0, vl)
+                model.set_gemm_variant(1, vr)
+                step()
+                abg.setdefault(f"{vl}:{vr}", []).append(
+                    round(n_global * args.steps / timed(step, args.steps), 1))
+        model.set_gemm_variant(0, 0)
+        model.set_gemm_variant(1, 0)
+        abg = {k: dict(runs=v, median=statistics.median(v)) for k, v in abg.items()}
     abf = None
     if args.ab_fold:
         m0 = load_model(args.model, dev, args.dtype, options={"ln_fold": False})
@@ -437,6 +454,8 @@ def run(args, backend="nccl", load_model=None):
             line["splits_ab_img_s"] = ab
         if abf:
             line["fold_ab_img_s"] = abf
+        if abg:
+            line["gemm_ab_img_s"] = abg
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

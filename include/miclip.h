@@ -237,6 +237,12 @@ int64_t miclip_model_bytes(const miclip_model* m);
 #define MICLIP_MODEL_MX_OUT 16
 #define MICLIP_MODEL_MX_GELU_TANH 32
 int miclip_model_flags(const miclip_model* m);
+/* Diagnostics: the GEMM kernel of the full-batch launches (>= 16384 rows) --
+ * which 0: the folded-LN store GEMMs (QKV, c_fc), 1: the fp16 residual GEMMs
+ * (out-proj, c_proj); variant 0 (default) / 259 (the 8-wave persistent kernel) /
+ * 508, 516 (the 4-wave gemm4s kernel). All are bit-identical, so results never
+ * change; bench.py --ab-gemm times them in one process. */
+int miclip_set_gemm_variant(miclip_model* m, int32_t which, int32_t variant);
 /* Switches a run-time option of a handle (only MICLIP_OPT_FULL_LAST_BLOCK; the
  * others fix the weight layout at create and return MICLIP_EINVAL). */
 int miclip_model_set_option(miclip_model* m, uint32_t option, int32_t on);

@@ -25,6 +25,7 @@ for step in "$@"; do
     ops4s)   run ops4s 400 python scripts/bench_ops.py --ops gemm --variants 259,508,516,259,508,516 --iters 20 ;;
     diag4s)  run diag4s 400 python scripts/bench_ops.py --ops gemm --only fc,proj --variants 508,508d,508e,259,259d,508,508d,508e,259 --iters 20 ;;
     spread)  run spread 400 python scripts/bench_ops.py --ops gemm --only fc,proj --variants 259,508,530,531,532,533,534,259,508,530,531,532,533,534 --iters 20 ;;
+    abgemm)  run abgemm 500 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-profile --ab-gemm 0:0,508:0,516:0,508:508 ;;
     lnfix)   run lnfix 600 $PYT tests/test_gpu_lnfold.py tests/test_gpu_openclip.py tests/test_gpu_parity.py -k "benched or head or zero_shot" ;;
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   run bench 400 python bench.py --steps 10 --warmup 3 --cpu-seconds 5 ;;
