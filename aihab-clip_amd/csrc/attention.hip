@@ -745,6 +745,9 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
   MICLIP_STAMP_END(blockIdx.x * 8 + wave);
 }
 
+#ifdef MICLIP_EXPERIMENTS
+// Experimental (measured level with the x8 kernel): built only into
+// the diagnostic library (make exp), never into the product libmiclip.so.
 // ---------------------------------------------------------------------------
 // Streamed form of the x8 kernel (variant 9; N in 257..259, head dim 64). The
 // x8 kernel stages a head's whole K/V image (66 KiB) before any wave computes,
@@ -1054,6 +1057,8 @@ __global__ __launch_bounds__(512, 4) void attention_stream_kernel(const T* __res
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+#endif  // MICLIP_EXPERIMENTS
+
 // ---------------------------------------------------------------------------
 // One query per (image, head): token row 0 (CLS) only. The vision tower's last
 // block feeds nothing but the CLS rows forward (VisionTransformer.forward,
@@ -1199,6 +1204,7 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, 
   // ragged one: K/V (72 KiB) plus the partials of 8 waves x the ragged queries
   // must stay under 80 KiB of LDS, i.e. N - 256 <= 3)
   const size_t lds_x8 = lds + (size_t)8 * (N > 256 ? N - 256 : 0) * 66 * 4;
+#ifdef MICLIP_EXPERIMENTS
   if (variant == 9) {
     // streamed x8 (attention_stream_kernel): N in 257..259, R key-tile slots
     if (CAUSAL || N < 257 || N > 259) return hipErrorInvalidValue;
@@ -1242,6 +1248,8 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, 
                          B, N, H, Npad, hpw, 0.125f, attn_prio());
     return hipGetLastError();
   }
+#endif  // MICLIP_EXPERIMENTS
+  if (variant == 9) return hipErrorInvalidValue;   // experiments build only
   if (variant == 8 || (!CAUSAL && variant == 0 && N >= 256 && N < 288 && lds_x8 <= 80 * 1024)) {
     // at most 3 ragged queries: one per merging wave (attention_x8_kernel)
     if (CAUSAL || N < 256 || N > 259 || lds_x8 > 80 * 1024) return hipErrorInvalidValue;

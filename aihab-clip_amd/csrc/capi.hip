@@ -1050,8 +1050,13 @@ int miclip_model_flags(const miclip_model* m) {
 
 int miclip_set_gemm_variant(miclip_model* m, int32_t which, int32_t variant) {
   if (!m || which < 0 || which > 1) return fail(MICLIP_EINVAL, "bad argument to set_gemm_variant");
+#ifdef MICLIP_EXPERIMENTS
   if (variant != 0 && variant != 259 && variant != 508 && variant != 516)
     return fail(MICLIP_EINVAL, "gemm variant must be 0, 259, 508 or 516 (bit-identical kernels)");
+#else
+  if (variant != 0 && variant != 259)
+    return fail(MICLIP_EINVAL, "gemm variant must be 0 or 259 (508 / 516: experiments library)");
+#endif
   m->gemm_variant[which] = variant;
   return 0;
 }

@@ -1352,6 +1352,10 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
   MICLIP_STAMP_END(blockIdx.x * 8 + wave);
 }
 
+#ifdef MICLIP_EXPERIMENTS
+// Experimental kernels (measured slower than the defaults): built
+// only into the diagnostic library (make exp -> build/exp/libmiclip_exp.so), never
+// into the product libmiclip.so.
 // ---------------------------------------------------------------------------
 // gemm4s: 256x256 tiles, 256 threads = 4 waves (2 x 2), 128 x 128 outputs per
 // wave -- ONE wave per SIMD with the 512-register budget: its 8 x 8 grid of
@@ -1703,6 +1707,8 @@ __global__ __launch_bounds__(256, 1) void gemm4s_kernel(const T* __restrict__ A,
   }
 }
 
+#endif  // MICLIP_EXPERIMENTS
+
 // ---------------------------------------------------------------------------
 // Persistent form of the staggered 256x256 kernel (SCHED 2): one workgroup per
 // CU walks its tiles (ids blockIdx.x + i*gridDim.x, so every round covers the
@@ -1904,6 +1910,10 @@ __global__ __launch_bounds__(512) void gemm256p_kernel(const T* __restrict__ A,
   }
   if (wr == 0) lds_barrier();   // balance the stagger barrier
 }
+#ifdef MICLIP_EXPERIMENTS
+// Experimental kernels (measured slower than the defaults): built
+// only into the diagnostic library (make exp -> build/exp/libmiclip_exp.so), never
+// into the product libmiclip.so.
 // ---------------------------------------------------------------------------
 // 256x256 tile, 256 threads = 4 waves (2x2), 128x128 per wave: ONE wave per
 // SIMD, its 8x8 grid of 16x16 fp32 fragments (256 registers) in the AGPR half
@@ -2487,6 +2497,8 @@ __global__ __launch_bounds__(256, 2) void gemm_pp_kernel(const T* __restrict__ A
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+#endif  // MICLIP_EXPERIMENTS
+
 // Kernel variants and schedule switches are chosen by the op-level `variant`
 // argument only (miclip_op_gemm: A/B benches); the model path runs variant 0,
 // which picks by problem size. The library reads no environment variables.
@@ -2576,6 +2588,7 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
       !(variant >= 400 && variant < 420) && variant != 508 && variant != 516 &&
       !(variant >= 530 && variant <= 534))
     return hipErrorInvalidValue;
+#ifdef MICLIP_EXPERIMENTS
   if constexpr (TrAcc<Epi>::value && !std::is_same_v<Epi, EpiResidual<float>>) {
     // ping-pong kernel: variant 400 + d = start delay of the second workgroup per
     // CU in microseconds
@@ -2665,8 +2678,17 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
       return hipGetLastError();
     }
   }
-  if (variant == 508 || variant == 516 || (variant >= 530 && variant <= 534))
-    return hipErrorInvalidValue;   // not applicable here
+  if (variant == 2) {   // 256x128, two workgroups per CU
+    const int tiles = ((M + 255) / 256) * (N / 128);
+    hipLaunchKernelGGL((gemm_t2_kernel<T, Epi>), dim3(tiles), dim3(256), 0, s, (const T*)A,
+                       (const T*)W, M, N, K, epi);
+    return hipGetLastError();
+  }
+#endif  // MICLIP_EXPERIMENTS
+  // experimental variants: refused here (not applicable, or not in this build)
+  if ((variant >= 400 && variant < 420) || variant == 300 || variant == 2 || variant == 508 ||
+      variant == 516 || (variant >= 530 && variant <= 534))
+    return hipErrorInvalidValue;
   // default for full-size problems: the persistent staggered kernel (variant
   // 259; same-process A/B vs 258 on the ViT-L/14 shapes: QKV +1 %, out-proj +9 %,
   // c_fc +1 %, c_proj +1 %)
@@ -2719,12 +2741,7 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
       return hipGetLastError();
     }
   }
-  if (variant == 2) {   // 256x128, two workgroups per CU
-    const int tiles = ((M + 255) / 256) * (N / 128);
-    hipLaunchKernelGGL((gemm_t2_kernel<T, Epi>), dim3(tiles), dim3(256), 0, s, (const T*)A,
-                       (const T*)W, M, N, K, epi);
-    return hipGetLastError();
-  }
+
   // Large problems: 256x256 tile (1 WG/CU, L2-friendly arithmetic intensity);
   // small ones (text tower, tiny batches) keep more workgroups with 128x128.
   const int tiles256 = ((M + 255) / 256) * (N / 256);

@@ -9,6 +9,10 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MICLIP_LIB", os.path.join(_HERE, "libmiclip.so"))
+# the diagnostic library with the measured-slower experimental kernels (make exp);
+# tests of those kernels and A/B scripts load it explicitly
+EXP_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "build", "exp",
+                            "libmiclip_exp.so")
 
 ABI_VERSION = 7          # include/miclip.h MICLIP_ABI_VERSION
 MICLIP_FP16 = 0
@@ -138,6 +142,11 @@ def load_library(path: str = None):
     if path is None:
         _lib = lib
     return lib
+
+
+def load_experiments():
+    """The experiments library (a separate handle; raises MiclipError if not built)."""
+    return load_library(EXP_LIB_PATH)
 
 
 def check(rc: int, what: str = ""):

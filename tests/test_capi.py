@@ -83,3 +83,15 @@ def test_abi_version_and_validation(lib):
                                 transformer_layers=12, compute_dtype=0, act=1, options=1 << 9)
     assert lib.miclip_model_create(ctypes.byref(bad_opt), 0, ctypes.byref(h)) == -1
     assert b"options" in lib.miclip_last_error()
+
+
+def test_product_library_has_no_experimental_kernels():
+    """The measured-slower experimental kernels (ping-pong / 256x128 / 4-wave GEMMs,
+    streamed attention) are fenced into build/exp/libmiclip_exp.so (make exp); the
+    product libmiclip.so does not contain them."""
+    from miclip import _lib
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gemm256s_kernel" in data
+    for name in (b"gemm_pp_kernel", b"gemm_t2_kernel", b"gemm4w_kernel", b"gemm4s_kernel",
+                 b"attention_stream_kernel"):
+        assert name not in data, name

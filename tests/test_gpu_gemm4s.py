@@ -27,7 +27,7 @@ def lib():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     from miclip import _lib
-    return _lib.load_library()
+    return _lib.load_experiments()   # measured-slower kernel: diagnostic library only
 
 
 def _stream():
