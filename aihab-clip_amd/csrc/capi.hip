@@ -536,7 +536,7 @@ int ensure_aux(miclip_model* m, int n) {
 
 // encode_image for B images whose workspace window is `w` (clip/model.py:216-235)
 int encode_image_part(miclip_model* m, Workspace w, const void* images, int in_dt, int B,
-                      float* out, uint32_t flags, hipStream_t s) {
+                      void* out, uint32_t flags, hipStream_t s) {
   const auto& c = m->cfg;
   const int P = c.vision_patch_size, R = c.image_resolution, W = c.vision_width;
   const int dh = c.vision_head_dim, g = R / P, np = g * g, N = np + 1, H = W / dh;
@@ -576,16 +576,23 @@ int encode_image_part(miclip_model* m, Workspace w, const void* images, int in_d
   // compact CLS block xc
   const void* xcls = cls_last ? w.xc : w.x;
   const int cstride = cls_last ? 1 : N;
+  // half-precision features (MICLIP_FLAG_OUT_FP16 / _BF16, the reference's fp16
+  // f{v}.pth files): the fp32 head result, rounded once (RNE) into `out`; the
+  // fp32 result goes through the c_fc buffer, free by now
+  const int odt = (flags & MICLIP_FLAG_OUT_FP16) ? kF16 : (flags & MICLIP_FLAG_OUT_BF16) ? kBF16 : -1;
+  float* o32 = odt < 0 ? (float*)out : proj ? (float*)w.f : w.feat;
+  const int dim = proj ? c.embed_dim : W;
   ProfScope p(m, K_HEAD, s, proj ? 2.0 * B * W * c.embed_dim : 0.0, (double)B * W * 8);
   if (!proj) {
-    MICLIP_HIP(layernorm(dt, xcls, nullptr, cstride, m->ln_post_g, m->ln_post_b, out, nullptr, B,
+    MICLIP_HIP(layernorm(dt, xcls, nullptr, cstride, m->ln_post_g, m->ln_post_b, o32, nullptr, B,
                          W, norm ? 1 : 0, s, m->resid16));
   } else {
     MICLIP_HIP(layernorm(dt, xcls, nullptr, cstride, m->ln_post_g, m->ln_post_b, w.feat, nullptr,
                          B, W, 0, s, m->resid16));
-    MICLIP_HIP(rowvec_matmul(w.feat, m->vproj, out, B, W, c.embed_dim, s));
-    if (norm) MICLIP_HIP(row_l2norm(out, B, c.embed_dim, s));
+    MICLIP_HIP(rowvec_matmul(w.feat, m->vproj, o32, B, W, c.embed_dim, s));
+    if (norm) MICLIP_HIP(row_l2norm(o32, B, c.embed_dim, s));
   }
+  if (odt >= 0) MICLIP_HIP(cast_pad(odt, o32, out, B, dim, dim, s));
   return 0;
 }
 
@@ -823,12 +830,20 @@ static int image_splits(const miclip_model* m, int B, int N) {
 
 int miclip_encode_image(miclip_model* m, const float* images, int32_t B, float* out,
                         uint32_t flags, void* stream) {
+  if (flags & (MICLIP_FLAG_OUT_FP16 | MICLIP_FLAG_OUT_BF16))
+    return fail(MICLIP_EINVAL, "miclip_encode_image writes fp32 (use miclip_encode_image_ex)");
   return miclip_encode_image_ex(m, images, MICLIP_F32, B, out, flags, stream);
 }
 
 int miclip_encode_image_ex(miclip_model* m, const void* images, int32_t image_dtype, int32_t B,
-                           float* out, uint32_t flags, void* stream) {
+                           void* out, uint32_t flags, void* stream) {
   if (!m || !images || !out || B < 1) return fail(MICLIP_EINVAL, "bad argument to encode_image");
+  if (flags & ~(MICLIP_FLAG_NORMALIZE | MICLIP_FLAG_APPLY_PROJ | MICLIP_FLAG_OUT_FP16 |
+                MICLIP_FLAG_OUT_BF16))
+    return fail(MICLIP_EINVAL, "unknown encode_image flags");
+  if ((flags & MICLIP_FLAG_OUT_FP16) && (flags & MICLIP_FLAG_OUT_BF16))
+    return fail(MICLIP_EINVAL, "MICLIP_FLAG_OUT_FP16 and MICLIP_FLAG_OUT_BF16 exclude each other");
+  const size_t out_bytes = (flags & (MICLIP_FLAG_OUT_FP16 | MICLIP_FLAG_OUT_BF16)) ? 2 : 4;
   if (image_dtype != MICLIP_F32 && image_dtype != MICLIP_FP16 && image_dtype != MICLIP_BF16)
     return fail(MICLIP_EINVAL, "image_dtype must be MICLIP_F32, MICLIP_FP16 or MICLIP_BF16");
   const int in_dt = image_dtype == MICLIP_F32 ? kIn32 : image_dtype == MICLIP_FP16 ? kF16 : kBF16;
@@ -860,7 +875,7 @@ int miclip_encode_image_ex(miclip_model* m, const void* images, int32_t image_dt
     if (p > 0) MICLIP_HIP(hipStreamWaitEvent(sp, m->ev_fork, 0));
     if ((rc = encode_image_part(m, view(m, m->wimg, (size_t)b0 * N, b0, N, W, p),
                                 (const char*)images + (size_t)b0 * 3 * R * R * in_bytes, in_dt,
-                                nb, out + (size_t)b0 * dim, flags, sp)))
+                                nb, (char*)out + (size_t)b0 * dim * out_bytes, flags, sp)))
       return rc;
     b0 += nb;
   }

@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("MICLIP_LIB", os.path.join(_HERE, "libmiclip.so"))
 EXP_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "build", "exp",
                             "libmiclip_exp.so")
 
-ABI_VERSION = 7          # include/miclip.h MICLIP_ABI_VERSION
+ABI_VERSION = 8          # include/miclip.h MICLIP_ABI_VERSION
 MICLIP_FP16 = 0
 MICLIP_BF16 = 1
 MICLIP_MXFP8 = 2
@@ -23,6 +23,8 @@ MICLIP_ACT_QUICKGELU = 1
 MICLIP_ACT_GELU = 2
 MICLIP_FLAG_NORMALIZE = 1
 MICLIP_FLAG_APPLY_PROJ = 2
+MICLIP_FLAG_OUT_FP16 = 4
+MICLIP_FLAG_OUT_BF16 = 8
 MICLIP_MODEL_RESID16 = 1
 MICLIP_MODEL_LNFOLD = 2
 MICLIP_MODEL_MXFP8 = 4

@@ -23,9 +23,12 @@ and the multi-GPU variant:
   * ShardedBatchLoader / gather_shards (per_rank=True): each rank reads and
     decodes only its own slice of every global batch.
 
-Differences that matter to callers: features are fp32 (the reference's GPU
-path returns fp16); the encode itself runs in the C ABI, with the optional
-normalise fused into ln_post.
+Differences that matter to callers: compute_image_features returns fp32 by
+default (the reference's GPU path returns the fp16 model's dtype; pass
+out_dtype=torch.float16 for that); the pre-projection cache f{v}.pth is fp16 as
+the reference writes it (cfg "cache_dtype": "fp16" default, "fp32" / "bf16");
+the encode itself runs in the C ABI, with the optional normalise and the output
+rounding fused into its head.
 """
 import json
 from datetime import datetime
@@ -80,6 +83,32 @@ def _feature_cache_exists(cache_dir: Path, aug_views: int) -> bool:
     if not cache_dir.exists() or not (cache_dir / "label.pth").is_file():
         return False
     return all((cache_dir / f"f{v}.pth").is_file() for v in range(aug_views))
+
+
+_CACHE_DTYPES = {"fp16": torch.float16, "float16": torch.float16, "half": torch.float16,
+                 "fp32": torch.float32, "float32": torch.float32, "float": torch.float32,
+                 "bf16": torch.bfloat16, "bfloat16": torch.bfloat16}
+
+
+def _cache_dtype(name, default: str) -> torch.dtype:
+    if name is None:
+        name = default
+    if isinstance(name, torch.dtype):
+        return name
+    try:
+        return _CACHE_DTYPES[str(name).lower()]
+    except KeyError:
+        raise ValueError(f"unknown cache dtype {name!r} (fp16, fp32 or bf16)") from None
+
+
+def _encode(clip_model, images, out_dtype=None, **kw):
+    """encode_image with the output element type fused into the HIP head where the
+    model is a miclip model; other models' features are cast."""
+    if out_dtype is None:
+        return clip_model.encode_image(images, **kw)
+    if hasattr(clip_model, "zero_shot"):
+        return clip_model.encode_image(images, out_dtype=out_dtype, **kw)
+    return clip_model.encode_image(images, **kw).to(out_dtype)
 
 
 def _model_device(clip_model):
@@ -156,15 +185,17 @@ def prepare_images(model, images, device):
 
 
 @torch.no_grad()
-def compute_image_features(clip_model, loader, to_cpu: bool = False):
+def compute_image_features(clip_model, loader, to_cpu: bool = False, out_dtype=None):
     """Pre-projection features and labels of every batch (methods/utils.py:142-173).
 
     With to_cpu the per-batch host copies are asynchronous (AsyncHostSink);
-    loaders may also yield decoded uint8 images (prepare_images)."""
+    loaders may also yield decoded uint8 images (prepare_images). out_dtype
+    (torch.float16 / bfloat16) rounds the features in the encode's own head
+    launch sequence (fp32 by default)."""
     device = _model_device(clip_model)
     feats, labels = ([], []) if not to_cpu else (AsyncHostSink(), [])
     for images, target in loader:
-        x = clip_model.encode_image(prepare_images(clip_model, images, device))
+        x = _encode(clip_model, prepare_images(clip_model, images, device), out_dtype)
         if to_cpu:
             feats.push(x)
             labels.append(target.detach().to("cpu"))
@@ -216,6 +247,8 @@ def cache_openclip_embeddings(cfg: dict, model, loader, split: str = "test",
     import pandas as pd
     ft = cfg.get("finetune", {}) or {}
     normalize = bool(ft.get("cache_embeddings_normalize", True))
+    # open_clip's model is fp32 in the reference (embeddings.pt fp32)
+    out_dtype = _cache_dtype(ft.get("cache_embeddings_dtype"), "fp32")
     cache_dir = _embedding_cache_dir(cfg, split)
     cache_dir.mkdir(parents=True, exist_ok=True)
     device = _model_device(model)
@@ -231,11 +264,12 @@ def cache_openclip_embeddings(cfg: dict, model, loader, split: str = "test",
             raise ValueError("Expected batch to be (images, targets) or (images, targets, metadata).")
         images = prepare_images(model, images, device)
         if hasattr(model, "zero_shot"):          # miclip model: normalise fused into ln_post
-            feats = model.encode_image(images, normalize=normalize)
+            feats = model.encode_image(images, normalize=normalize, out_dtype=out_dtype)
         else:
             feats = model.encode_image(images)
             if normalize:
                 feats = F.normalize(feats, dim=-1)
+            feats = feats.to(out_dtype)
         sink.push(feats)
         t = targets.detach().to("cpu")
         labels_list.append(t)
@@ -263,23 +297,30 @@ def cache_openclip_embeddings(cfg: dict, model, loader, split: str = "test",
 
 @torch.no_grad()
 def cache_preprojection_features(cfg, clip_bundle: dict, dl_tr, info: dict):
-    """f{v}.pth per augmentation view + label.pth (aihab_utils/feature_cache.py:189-250)."""
+    """f{v}.pth per augmentation view + label.pth (aihab_utils/feature_cache.py:189-250).
+
+    The features are fp16 like the reference's (its clip.load(..., device="cuda")
+    model is fp16, so compute_image_features returns fp16, :211); cfg
+    "cache_dtype" "fp32" / "bf16" picks another element type."""
     clip_model = clip_bundle["clip_model"]
     cache_dir = _feature_cache_dir(cfg)
     num_views = int(cfg.get("aug_views", 1) or 1)
+    out_dtype = _cache_dtype(cfg.get("cache_dtype"), "fp16")
     expected_n = info.get("train_size") if info else None
     if expected_n is None and hasattr(dl_tr, "dataset"):
         expected_n = len(dl_tr.dataset)
     clip_model.eval()
     for v in range(num_views):
-        feats_t, labels_t = compute_image_features(clip_model, dl_tr, to_cpu=True)
+        feats_t, labels_t = compute_image_features(clip_model, dl_tr, to_cpu=True,
+                                                   out_dtype=out_dtype)
         fpath = cache_dir / f"f{v}.pth"
         fpath.parent.mkdir(parents=True, exist_ok=True)
         torch.save(feats_t, fpath)
         if v == 0:
             torch.save(labels_t, cache_dir / "label.pth")
         loaded = torch.load(fpath, map_location="cpu", weights_only=True)
-        print({"view": v, "reload_shape_ok": tuple(loaded.shape) == tuple(feats_t.shape),
+        print({"view": v, "features.dtype": str(feats_t.dtype),
+               "reload_shape_ok": tuple(loaded.shape) == tuple(feats_t.shape),
                "rows_match_labels": feats_t.shape[0] == labels_t.shape[0],
                "rows_match_expected": expected_n is None or feats_t.shape[0] == int(expected_n)})
     return cache_dir

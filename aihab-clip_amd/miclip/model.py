@@ -41,6 +41,8 @@ from . import _lib
 from .configs import CLIPConfig
 
 # "mxfp8": QKV / c_fc / c_proj on MX-fp8 operands, fp16 elsewhere
+_OUT_FLAGS = {torch.float32: 0, torch.float16: _lib.MICLIP_FLAG_OUT_FP16,
+              torch.bfloat16: _lib.MICLIP_FLAG_OUT_BF16}
 _DTYPES = {"fp16": (_lib.MICLIP_FP16, torch.float16), "float16": (_lib.MICLIP_FP16, torch.float16),
            "bf16": (_lib.MICLIP_BF16, torch.bfloat16), "bfloat16": (_lib.MICLIP_BF16, torch.bfloat16),
            "mxfp8": (_lib.MICLIP_MXFP8, torch.float16)}
@@ -290,7 +292,7 @@ class CLIP(nn.Module):
                                   "PEFT training is not supported")
 
     @torch.no_grad()
-    def encode_image(self, image, normalize=False, apply_proj=None, out=None):
+    def encode_image(self, image, normalize=False, apply_proj=None, out=None, out_dtype=None):
         """Pre-projection image features [B, vision_width] (clip/model.py:335-336, 216-235);
         post-projection [B, embed_dim] on the open_clip surface (open_clip's
         `encode_image(image, normalize=False)`, methods/PEFT_openclip.py:90-92).
@@ -298,7 +300,11 @@ class CLIP(nn.Module):
         normalize / apply_proj fuse the callers' F.normalize
         (aihab_utils/feature_cache.py:126-127) and `@ visual.proj`
         (methods/ProLIP.py:38-41) into the same launch sequence; apply_proj
-        defaults to the surface's contract.
+        defaults to the surface's contract. out_dtype torch.float32 (default),
+        torch.float16 -- the reference GPU path's element type (clip.load on cuda
+        keeps the model fp16), so cached f{v}.pth files match its dtype and size --
+        or torch.bfloat16: the fp32 result rounded once, in the same launch
+        sequence (MICLIP_FLAG_OUT_FP16 / _BF16).
         """
         h = self._require()
         if apply_proj is None:
@@ -316,15 +322,18 @@ class CLIP(nn.Module):
                        dtype=image.dtype if in_dt != _lib.MICLIP_F32 else torch.float32).contiguous()
         B = img.shape[0]
         dim = self.config.embed_dim if apply_proj else self.config.vision_width
+        odt = out_dtype if out_dtype is not None else (out.dtype if out is not None else torch.float32)
+        oflag = _OUT_FLAGS.get(odt)
+        if oflag is None:
+            raise ValueError(f"out_dtype must be torch.float32, float16 or bfloat16, got {odt}")
         if out is None:
-            out = torch.empty(B, dim, device=self.device, dtype=torch.float32)
-        elif out.shape != (B, dim) or out.dtype != torch.float32 or not out.is_contiguous():
-            raise ValueError("out must be a contiguous float32 tensor of shape "
-                             f"({B}, {dim})")
+            out = torch.empty(B, dim, device=self.device, dtype=odt)
+        elif out.shape != (B, dim) or out.dtype != odt or not out.is_contiguous():
+            raise ValueError(f"out must be a contiguous {odt} tensor of shape ({B}, {dim})")
         if B == 0:
             return out
         flags = (_lib.MICLIP_FLAG_NORMALIZE if normalize else 0) | \
-                (_lib.MICLIP_FLAG_APPLY_PROJ if apply_proj else 0)
+                (_lib.MICLIP_FLAG_APPLY_PROJ if apply_proj else 0) | oflag
         with torch.cuda.device(self.device):
             _lib.check(h.lib.miclip_encode_image_ex(h.ptr, img.data_ptr(), in_dt, B, out.data_ptr(),
                                                     flags, _lib.stream_handle(self.device)),

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MICLIP_ABI_VERSION 7
+#define MICLIP_ABI_VERSION 8
 
 enum miclip_status {
   MICLIP_OK = 0,
@@ -51,6 +51,13 @@ enum miclip_act { MICLIP_ACT_QUICKGELU = 1, MICLIP_ACT_GELU = 2, MICLIP_ACT_GELU
 /* encode_image flags */
 #define MICLIP_FLAG_NORMALIZE 1u  /* F.normalize(feats, dim=-1): aihab_utils/feature_cache.py:126-127 */
 #define MICLIP_FLAG_APPLY_PROJ 2u /* feats @ visual.proj:       methods/ProLIP.py:38-41 */
+/* miclip_encode_image_ex only: `out` holds fp16 (or bf16) features, the fp32
+ * result rounded once (RNE) -- the element type of the reference's GPU path
+ * (clip.load on cuda keeps the model fp16, so encode_image returns fp16 and the
+ * cached f{v}.pth / embeddings.pt are fp16: aihab_utils/feature_cache.py:126-131,
+ * 208-222). The two exclude each other. */
+#define MICLIP_FLAG_OUT_FP16 4u
+#define MICLIP_FLAG_OUT_BF16 8u
 
 /* Model hyper-parameters; the fields of clip/model.py:240-254 (CLIP.__init__),
  * as inferred by build_model (clip/model.py:396-419). ViT towers only. */
@@ -122,7 +129,8 @@ int miclip_reserve(miclip_model* m, int32_t max_images, int32_t max_prompts);
  * 216-235). images: device fp32 [B,3,R,R] (CLIP-normalised, clip/clip.py:80).
  * out: device fp32 [B, vision_width] pre-projection features (the modified
  * reference returns ln_post(x[:,0,:]) without @proj, clip/model.py:228-235), or
- * [B, embed_dim] with MICLIP_FLAG_APPLY_PROJ; MICLIP_FLAG_NORMALIZE L2-normalises. */
+ * [B, embed_dim] with MICLIP_FLAG_APPLY_PROJ; MICLIP_FLAG_NORMALIZE L2-normalises.
+ * fp32 out only (the OUT_FP16 / OUT_BF16 flags are miclip_encode_image_ex's). */
 int miclip_encode_image(miclip_model* m, const float* images, int32_t B, float* out,
                         uint32_t flags, void* stream);
 
@@ -130,9 +138,11 @@ int miclip_encode_image(miclip_model* m, const float* images, int32_t B, float* 
  * image_dtype MICLIP_F32, MICLIP_FP16 or MICLIP_BF16 (a device-resident half
  * batch, e.g. the reference's `images.to(device).half()` under clip.load on GPU,
  * clip/model.py:336 `image.type(self.dtype)`, read directly by the patchify:
- * half the input bytes of fp32). Same outputs and flags. */
+ * half the input bytes of fp32). Same outputs and flags, plus MICLIP_FLAG_OUT_FP16 /
+ * MICLIP_FLAG_OUT_BF16: `out` is then [B, dim] 2-byte elements. Unknown flag
+ * bits: MICLIP_EINVAL. */
 int miclip_encode_image_ex(miclip_model* m, const void* images, int32_t image_dtype, int32_t B,
-                           float* out, uint32_t flags, void* stream);
+                           void* out, uint32_t flags, void* stream);
 
 /* Replaces CLIP.encode_text (clip/model.py:338-353), which returns the tuple
  * (x_before_proj [P, transformer_width], x [P, embed_dim]). tokens: device

@@ -52,7 +52,7 @@ def test_nm_shows_c_linkage():
 
 def test_abi_version_and_validation(lib):
     from miclip import _lib
-    assert lib.miclip_abi_version() == _lib.ABI_VERSION == 7
+    assert lib.miclip_abi_version() == _lib.ABI_VERSION == 8
     bad = _lib.MiclipConfig(embed_dim=512, image_resolution=224, vision_layers=12, vision_width=700,
                             vision_patch_size=32, context_length=77, vocab_size=49408,
                             transformer_width=512, transformer_heads=8, transformer_layers=12,

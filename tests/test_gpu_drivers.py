@@ -199,7 +199,8 @@ def test_cache_openclip_embeddings_layout(golden, tmp_path):
 
 
 def test_cache_preprojection_features_layout(golden, tmp_path):
-    from miclip.feature_cache import _feature_cache_exists, cache_preprojection_features
+    from miclip.feature_cache import (_feature_cache_exists, cache_preprojection_features,
+                                      compute_image_features)
     from miclip.weights import synthetic_images
     g = golden("vitb32")
     n = g["meta"]["n_images"]
@@ -214,9 +215,37 @@ def test_cache_preprojection_features_layout(golden, tmp_path):
     f0 = torch.load(d / "f0.pth", weights_only=True)
     f1 = torch.load(d / "f1.pth", weights_only=True)
     lab = torch.load(d / "label.pth", weights_only=True)
-    assert f0.dtype == torch.float32 and f0.shape == (n, 768)
-    assert _one_minus_cos(f0, g["image"]).max() <= COS_TOL      # pre-projection, not normalised
+    # fp16 like the reference's fp16 model writes them: the fp32 features rounded once
+    assert f0.dtype == torch.float16 and f0.shape == (n, 768)
+    assert _one_minus_cos(f0.float(), g["image"]).max() <= COS_TOL   # pre-projection, not normalised
     assert torch.equal(f0, f1) and torch.equal(lab, torch.from_numpy(labels))
+    f32, _ = compute_image_features(m, _loader(imgs, labels, 3), to_cpu=True)
+    assert torch.equal(f0, f32.half())
+    cfg32 = dict(cfg, cache_dtype="fp32", root_path=str(tmp_path / "f32"))
+    d32 = cache_preprojection_features(cfg32, {"clip_model": m}, _loader(imgs, labels, 3), None)
+    assert torch.equal(torch.load(d32 / "f0.pth", weights_only=True), f32)
+    with pytest.raises(ValueError):
+        cache_preprojection_features(dict(cfg, cache_dtype="int8"), {"clip_model": m},
+                                     _loader(imgs, labels, 3), None)
+
+
+@pytest.mark.parametrize("proj,norm", [(False, False), (True, True), (False, True)])
+def test_encode_image_out_dtype(golden, proj, norm):
+    """out_dtype fp16 / bf16: the fp32 features rounded once (RNE) in the head's
+    launch sequence -- bit for bit the fp32 result's .to(dtype), all paths."""
+    from miclip.weights import synthetic_images
+    g = golden("vitb32")
+    imgs = torch.from_numpy(synthetic_images(g["meta"]["n_images"], 224, seed=0)).cuda()
+    m = _model("ViT-B/32")
+    f32 = m.encode_image(imgs, normalize=norm, apply_proj=proj)
+    for dt in (torch.float16, torch.bfloat16):
+        h = m.encode_image(imgs, normalize=norm, apply_proj=proj, out_dtype=dt)
+        assert h.dtype == dt and torch.equal(h, f32.to(dt))
+        out = torch.empty_like(h)
+        assert m.encode_image(imgs, normalize=norm, apply_proj=proj, out=out) is out
+        assert torch.equal(out, h)
+    with pytest.raises(ValueError):
+        m.encode_image(imgs, out_dtype=torch.int8)
 
 
 def test_async_host_sink_depth_below_batches():
