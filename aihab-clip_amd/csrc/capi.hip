@@ -133,7 +133,7 @@ struct miclip_model {
   // miclip_set_gemm_variant for same-process A/B: [0] the folded-LN store GEMMs
   // (QKV, c_fc), [1] the fp16 residual GEMMs (out-proj, c_proj). 0 = default.
   // Only variants bit-identical to the default are accepted: results never change.
-  int gemm_variant[2] = {0, 0};
+  int gemm_variant[3] = {0, 0, 0};   // [2]: the MX-fp8 GEMMs (gemm_mx variant)
   // ln_1 / ln_2 folded into the QKV / c_fc GEMMs (fp16 stream models;
   // MICLIP_OPT_NO_LN_FOLD runs the LayerNorm kernels instead); folded weights are
   // rebuilt per tower after every weight load
@@ -400,7 +400,7 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
     ProfScope p(m, K_GEMM_QKV, s, gemm_flops(dM, 3 * dW, dW), gemm_bytes(dM, 3 * dW, dW, 2));
     if (mx)
       MICLIP_HIP(gemm_mx(w.hq, w.hs, b.w_qkv, b.s_qkv, b.b_qkv, w.qkv, nullptr, M, 3 * W, W, 0,
-                         ACT_NONE, s));
+                         ACT_NONE, s, m->gemm_variant[2]));
     else if (fold)
       MICLIP_HIP(gemm_store_ln(dt, w.x, b.wf_qkv, b.c_qkv, b.cs_qkv, w.stats, w.qkv, M, 3 * W, W,
                                ACT_NONE, s, vln));
@@ -418,7 +418,7 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
     if (b.s_out) {   // MX-fp8 out-proj (vision tower of an MX model)
       MICLIP_HIP(quant_mx(1, w.o, items, W, w.hq, w.hs, s));
       MICLIP_HIP(gemm_mx(w.hq, w.hs, b.w_out, b.s_out, b.b_out, w.xc, nullptr, items, W, W, 1,
-                         ACT_NONE, s));
+                         ACT_NONE, s, m->gemm_variant[2]));
     } else {
       MICLIP_HIP(gemm_residual(dt, w.o, b.w_out, b.b_out, w.xc, items, W, W, s, 0, r16));
     }
@@ -426,9 +426,9 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
       MICLIP_HIP(layernorm(dt, w.xc, nullptr, 1, b.ln2_g, b.ln2_b, nullptr, nullptr, items, W, 0,
                            s, r16, w.hq, w.hs));
       MICLIP_HIP(gemm_mx(w.hq, w.hs, b.w_fc, b.s_fc, b.b_fc, w.fq, w.fs, items, 4 * W, W, 5,
-                         mx_act(m, m->cfg.act), s));
+                         mx_act(m, m->cfg.act), s, m->gemm_variant[2]));
       MICLIP_HIP(gemm_mx(w.fq, w.fs, b.w_proj, b.s_proj, b.b_proj, w.xc, nullptr, items, W, 4 * W,
-                         1, ACT_NONE, s));
+                         1, ACT_NONE, s, m->gemm_variant[2]));
       return 0;
     }
     if (fold) {
@@ -453,7 +453,7 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
     if (b.s_out) {   // quantise the attention output (hq / hs are free here), MX GEMM
       MICLIP_HIP(quant_mx(1, w.o, M, W, w.hq, w.hs, s));
       MICLIP_HIP(gemm_mx(w.hq, w.hs, b.w_out, b.s_out, b.b_out, w.x, nullptr, M, W, W, 1,
-                         ACT_NONE, s));
+                         ACT_NONE, s, m->gemm_variant[2]));
     } else {
       MICLIP_HIP(gemm_residual(dt, w.o, b.w_out, b.b_out, w.x, M, W, W, s, r16 ? vres : 0, r16));
     }
@@ -475,7 +475,7 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
                 mx ? dM * dW + 4 * dW * dW + 4 * dM * dW : gemm_bytes(dM, 4 * dW, dW, 2));
     if (mx)
       MICLIP_HIP(gemm_mx(w.hq, w.hs, b.w_fc, b.s_fc, b.b_fc, w.fq, w.fs, M, 4 * W, W, 5,
-                         mx_act(m, m->cfg.act), s));
+                         mx_act(m, m->cfg.act), s, m->gemm_variant[2]));
     else if (fold)
       MICLIP_HIP(gemm_store_ln(dt, w.x, b.wf_fc, b.c_fc, b.cs_fc, w.stats, w.f, M, 4 * W, W,
                                m->cfg.act, s, vln));
@@ -488,7 +488,7 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
                    : gemm_bytes(dM, dW, 4 * dW, 2 * rb));
     if (mx)
       MICLIP_HIP(gemm_mx(w.fq, w.fs, b.w_proj, b.s_proj, b.b_proj, w.x, nullptr, M, W, 4 * W, 1,
-                         ACT_NONE, s));
+                         ACT_NONE, s, m->gemm_variant[2]));
     else
       MICLIP_HIP(gemm_residual(dt, w.f, b.w_proj, b.b_proj, w.x, M, W, 4 * W, s, r16 ? vres : 0,
                                r16));
@@ -1064,7 +1064,13 @@ int miclip_model_flags(const miclip_model* m) {
 }
 
 int miclip_set_gemm_variant(miclip_model* m, int32_t which, int32_t variant) {
-  if (!m || which < 0 || which > 1) return fail(MICLIP_EINVAL, "bad argument to set_gemm_variant");
+  if (!m || which < 0 || which > 2) return fail(MICLIP_EINVAL, "bad argument to set_gemm_variant");
+  if (which == 2) {   // MX-fp8 GEMMs: 0 default, 1 one tile per workgroup, 2 persistent
+    if (variant < 0 || variant > 2)
+      return fail(MICLIP_EINVAL, "MX gemm variant must be 0, 1 or 2 (bit-identical kernels)");
+    m->gemm_variant[2] = variant;
+    return 0;
+  }
 #ifdef MICLIP_EXPERIMENTS
   if (variant != 0 && variant != 259 && variant != 508 && variant != 516)
     return fail(MICLIP_EINVAL, "gemm variant must be 0, 259, 508 or 516 (bit-identical kernels)");
@@ -1175,6 +1181,14 @@ int miclip_op_gemm_mx(const void* A, const void* SA, const void* W, const void* 
                       int32_t epi, int32_t act, void* stream) {
   if (!A || !SA || !W || !SW || !C) return fail(MICLIP_EINVAL, "null argument");
   MICLIP_HIP(gemm_mx(A, SA, W, SW, bias, C, CS, M, N, K, epi, act, (hipStream_t)stream));
+  return 0;
+}
+
+int miclip_op_gemm_mx_v(const void* A, const void* SA, const void* W, const void* SW,
+                        const float* bias, void* C, void* CS, int32_t M, int32_t N, int32_t K,
+                        int32_t epi, int32_t act, int32_t variant, void* stream) {
+  if (!A || !SA || !W || !SW || !C) return fail(MICLIP_EINVAL, "null argument");
+  MICLIP_HIP(gemm_mx(A, SA, W, SW, bias, C, CS, M, N, K, epi, act, (hipStream_t)stream, variant));
   return 0;
 }
 

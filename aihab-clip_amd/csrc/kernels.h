@@ -50,8 +50,11 @@ hipError_t quant_mx(int in_f16, const void* in, int R, int K, void* q, void* sc,
 // C = A[M,K] . W[N,K]^T with MX-fp8 operands (N % 256 == 0, K % 128 == 0).
 // epi 0: C fp16 = act(acc + bias); epi 1: C fp16 residual += acc + bias;
 // epi 5: C MX-fp8 data [M, N] + scale plane CS = MX(act(acc + bias)).
+// variant: 0 persistent where it applies (K >= 256), 1 one tile per workgroup,
+// 2 persistent only (bit-identical kernels; A/B)
 hipError_t gemm_mx(const void* A, const void* SA, const void* W, const void* SW, const float* bias,
-                   void* C, void* CS, int M, int N, int K, int epi, int act, hipStream_t s);
+                   void* C, void* CS, int M, int N, int K, int epi, int act, hipStream_t s,
+                   int variant = 0);
 
 // ---- LayerNorm (fp32 statistics, eps 1e-5) over rows of width D ----
 // Row r of the input is at in + in_row(r)*D with in_row(r) = rows ? rows[r] : r*in_stride_rows;

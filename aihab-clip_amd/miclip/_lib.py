@@ -48,7 +48,7 @@ EXPORTS = (
     "miclip_op_gemm", "miclip_op_ln_stats", "miclip_op_ln_fold", "miclip_op_gemm_ln",
     "miclip_op_layernorm", "miclip_op_attention", "miclip_op_attention_q0", "miclip_preprocess",
     "miclip_row_norms", "miclip_class_centroids", "miclip_proto_scores",
-    "miclip_mx_scale_bytes", "miclip_op_quant_mx", "miclip_op_gemm_mx", "miclip_op_layernorm_mx",
+    "miclip_mx_scale_bytes", "miclip_op_quant_mx", "miclip_op_gemm_mx", "miclip_op_gemm_mx_v", "miclip_op_layernorm_mx",
 )
 
 MICLIP_PRE_F32 = 0
@@ -129,6 +129,8 @@ def load_library(path: str = None):
         "miclip_op_quant_mx": ([vp, i32, i32, i32, vp, vp, vp], ctypes.c_int),
         "miclip_op_gemm_mx": ([vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
                               ctypes.c_int),
+        "miclip_op_gemm_mx_v": ([vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp],
+                                ctypes.c_int),
         "miclip_op_layernorm_mx": ([vp, i32, vp, vp, vp, vp, i32, i32, vp], ctypes.c_int),
         "miclip_preprocess": ([vp, vp, ctypes.POINTER(MiclipImageDesc), i32, vp, i32, vp],
                               ctypes.c_int),

@@ -255,7 +255,8 @@ class CLIP(nn.Module):
 
     def set_gemm_variant(self, which, variant):
         """Diagnostics: kernel of the full-batch GEMM launches (which 0: QKV / c_fc,
-        1: out-proj / c_proj); bit-identical variants only (miclip_set_gemm_variant)."""
+        1: out-proj / c_proj, 2: every MX-fp8 GEMM); bit-identical variants only
+        (miclip_set_gemm_variant)."""
         h = self._require()
         _lib.check(h.lib.miclip_set_gemm_variant(h.ptr, int(which), int(variant)),
                    "miclip_set_gemm_variant")

@@ -69,8 +69,9 @@ def parse(argv=None):
     ap.add_argument("--splits", type=int, default=2, help="encode_image batch split over streams")
     ap.add_argument("--ab-splits", action="store_true", help="also time splits=1 vs 2 (diagnostic)")
     ap.add_argument("--ab-gemm", default="",
-                    help="diagnostic: also time these GEMM variant pairs 'ln:res,...' (e.g. "
-                         "'0:0,508:0') interleaved in this process (bit-identical kernels)")
+                    help="diagnostic: also time these GEMM variants 'ln:res[:mx],...' (e.g. "
+                         "'0:0,508:0' or '0:0:1,0:0:2' for the MX-fp8 kernels) interleaved in "
+                         "this process (bit-identical kernels)")
     ap.add_argument("--ab-fold", action="store_true",
                     help="also time a second model with options ln_fold=False in this process (diagnostic)")
     return ap.parse_args(argv)
@@ -350,14 +351,14 @@ def run(args, backend="nccl", load_model=None):
         abg = {}
         pairs = [tuple(int(x) for x in p.split(":")) for p in args.ab_gemm.split(",")]
         for _ in range(3):
-            for vl, vr in pairs:
-                model.set_gemm_variant(0, vl)
-                model.set_gemm_variant(1, vr)
+            for pv in pairs:
+                for which, v in enumerate(pv):      # ln:res[:mx]
+                    model.set_gemm_variant(which, v)
                 step()
-                abg.setdefault(f"{vl}:{vr}", []).append(
+                abg.setdefault(":".join(map(str, pv)), []).append(
                     round(n_global * args.steps / timed(step, args.steps), 1))
-        model.set_gemm_variant(0, 0)
-        model.set_gemm_variant(1, 0)
+        for which in range(3):
+            model.set_gemm_variant(which, 0)
         abg = {k: dict(runs=v, median=statistics.median(v)) for k, v in abg.items()}
     abf = None
     if args.ab_fold:

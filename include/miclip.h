@@ -250,8 +250,9 @@ int miclip_model_flags(const miclip_model* m);
 /* Diagnostics: the GEMM kernel of the full-batch launches (>= 16384 rows) --
  * which 0: the folded-LN store GEMMs (QKV, c_fc), 1: the fp16 residual GEMMs
  * (out-proj, c_proj); variant 0 (default) / 259 (the 8-wave persistent kernel) /
- * 508, 516 (the 4-wave gemm4s kernel). All are bit-identical, so results never
- * change; bench.py --ab-gemm times them in one process. */
+ * 508, 516 (the 4-wave gemm4s kernel); which 2: the MX-fp8 GEMMs (variants of
+ * miclip_op_gemm_mx_v). All are bit-identical, so results never change;
+ * bench.py --ab-gemm times them in one process. */
 int miclip_set_gemm_variant(miclip_model* m, int32_t which, int32_t variant);
 /* Switches a run-time option of a handle (only MICLIP_OPT_FULL_LAST_BLOCK; the
  * others fix the weight layout at create and return MICLIP_EINVAL). */
@@ -349,6 +350,12 @@ int miclip_op_quant_mx(const void* in, int32_t in_f16, int32_t R, int32_t K, voi
 int miclip_op_gemm_mx(const void* A, const void* SA, const void* W, const void* SW,
                       const float* bias, void* C, void* CS, int32_t M, int32_t N, int32_t K,
                       int32_t epi, int32_t act, void* stream);
+/* miclip_op_gemm_mx with the kernel named: variant 0 default (persistent where K >=
+ * 256), 1 one 256x256 tile per workgroup, 2 persistent (MICLIP_EINVAL where it does
+ * not apply). Bit-identical outputs (A/B and tests). */
+int miclip_op_gemm_mx_v(const void* A, const void* SA, const void* W, const void* SW,
+                        const float* bias, void* C, void* CS, int32_t M, int32_t N, int32_t K,
+                        int32_t epi, int32_t act, int32_t variant, void* stream);
 /* LayerNorm (fp32 in, or fp16 if in_f16) -> MX-fp8 rows q [R, D] + scales */
 int miclip_op_layernorm_mx(const void* in, int32_t in_f16, const float* gamma, const float* beta,
                            void* q, void* scales, int32_t R, int32_t D, void* stream);
