@@ -1,6 +1,7 @@
 #!/usr/bin/env python
-"""Eager vs HIP-graph-replayed encode_image at ViT-L/14 bs=256 (same process):
-whether launch gaps between the ~170 kernels per stream cost anything."""
+"""Eager vs HIP-graph-replayed encode_image (same process): whether launch gaps
+between the kernels cost anything.  graph_probe.py [B] [model] [dtype]
+(default 256 ViT-L/14 fp16; C2: 256 ViT-B/32 bf16)."""
 import os
 import sys
 import time
@@ -25,9 +26,12 @@ def timed(fn, n):
 
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
-    _, m, _ = miclip.load("ViT-L/14", device="cuda", compute_dtype="fp16")
+    name = sys.argv[2] if len(sys.argv) > 2 else "ViT-L/14"
+    dtype = sys.argv[3] if len(sys.argv) > 3 else "fp16"
+    _, m, _ = miclip.load(name, device="cuda", compute_dtype=dtype)
     m.reserve(B, 20)
-    x = torch.from_numpy(synthetic_images(B, 224, seed=1)).cuda()
+    R = m.config.image_resolution
+    x = torch.from_numpy(synthetic_images(B, R, seed=1)).cuda()
     eager_out = m.encode_image(x)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
