@@ -560,7 +560,7 @@ int encode_image_part(miclip_model* m, Workspace w, const void* images, int in_d
     ProfScope p(m, K_LAYERNORM, s, 0, (double)M * W * (m->resid16 ? 4 : 8));
     MICLIP_HIP(class_token(m->cls, m->vpos, w.x, B, N, W, s, m->resid16));
     // ln_pre in place: fp32 stream -> fp32 out; fp16 stream -> compute-dtype (fp16) out
-    MICLIP_HIP(layernorm(dt, w.x, nullptr, 1, m->ln_pre_g, m->ln_pre_b,
+    MICLIP_HIP(layernorm(m->resid16 ? kF16 : dt, w.x, nullptr, 1, m->ln_pre_g, m->ln_pre_b,
                          m->resid16 ? nullptr : (float*)w.x, m->resid16 ? w.x : nullptr, M, W,
                          0, s, m->resid16));
   }
@@ -661,8 +661,8 @@ int miclip_model_create(const miclip_config* cfg, int device, miclip_model** out
   // fp16 stream: every MX model (its text tower's folded path included), fp16
   // compute unless RESID_F32; LN fold on the fp16 stream unless NO_LN_FOLD (MX
   // vision blocks quantise the LayerNorm output instead: run_block)
-  m->resid16 = m->mx || (m->dtype == MICLIP_FP16 && !(o & MICLIP_OPT_RESID_F32));
-  m->lnfold = m->resid16 && !(o & MICLIP_OPT_NO_LN_FOLD);
+  m->resid16 = m->mx || !(o & MICLIP_OPT_RESID_F32);
+  m->lnfold = m->resid16 && m->dtype == MICLIP_FP16 && !(o & MICLIP_OPT_NO_LN_FOLD);
   const int P = cfg->vision_patch_size, Wv = cfg->vision_width, Wt = cfg->transformer_width;
   m->Kp = (3 * P * P + 63) / 64 * 64;
   const int g = cfg->image_resolution / P, N = g * g + 1, E = cfg->embed_dim;

@@ -2840,8 +2840,9 @@ hipError_t gemm_store_ln(int dtype, const void* A, const void* W, const float* c
 
 hipError_t gemm_residual(int dtype, const void* A, const void* W, const float* bias, void* X,
                          int M, int N, int K, hipStream_t s, int v, int resid16) {
-  if (resid16) {  // fp16 residual stream: fp16 compute only
-    if (dtype != kF16) return hipErrorInvalidValue;
+  if (resid16) {  // fp16 residual stream (fp16 or bf16 operands)
+    if (dtype == kBF16)
+      return launch<__bf16>(A, W, M, N, K, EpiResidual<_Float16>{(_Float16*)X, bias, N}, s, v);
     return launch<_Float16>(A, W, M, N, K, EpiResidual<_Float16>{(_Float16*)X, bias, N}, s, v);
   }
   if (dtype == kF16)
@@ -2864,8 +2865,9 @@ hipError_t gemm_null(int dtype, const void* A, const void* W, float* C, int M, i
 hipError_t gemm_patch(int dtype, const void* A, const void* W, const float* pos, void* X, int M,
                       int N, int K, int np, hipStream_t s, int resid16) {
   if (np <= 0 || M % np) return hipErrorInvalidValue;
-  if (resid16) {
-    if (dtype != kF16) return hipErrorInvalidValue;
+  if (resid16) {   // patch embedding into the fp16 stream (fp16 or bf16 operands)
+    if (dtype == kBF16)
+      return launch<__bf16>(A, W, M, N, K, EpiPatch<_Float16>{(_Float16*)X, pos, N, np}, s);
     return launch<_Float16>(A, W, M, N, K, EpiPatch<_Float16>{(_Float16*)X, pos, N, np}, s);
   }
   if (dtype == kF16)

@@ -409,7 +409,14 @@ hipError_t layernorm(int dtype, const void* in, const int32_t* rows, int in_stri
   if (R < 1 || D % 256 || D > 1536 || (!out_f32 && !out_t && !out_q)) return hipErrorInvalidValue;
   if (out_q && !out_s) return hipErrorInvalidValue;
   uint8_t *oq = (uint8_t*)out_q, *os = (uint8_t*)out_s;
-  if (in16) {  // fp16 residual stream: fp16 compute only
+  if (in16 && dtype == kBF16) {  // fp16 residual stream under bf16 compute: bf16 out
+    if (out_q) return hipErrorInvalidValue;   // MX output: the fp16 models only
+    if (out_t && !out_f32 && !rows && in_stride_rows == 1 && !normalize)
+      return ln_h2_dispatch<__bf16>((const _Float16*)in, gamma, beta, out_t, R, D, s);
+    return ln_dispatch<__bf16>((const _Float16*)in, rows, in_stride_rows, gamma, beta, out_f32,
+                               out_t, R, D, normalize, s, oq, os);
+  }
+  if (in16) {  // fp16 residual stream, fp16 compute (dtype = the out_t type)
     if (dtype != kF16) return hipErrorInvalidValue;
     if (out_t && !out_f32 && !out_q && !rows && in_stride_rows == 1 && !normalize)
       return ln_h2_dispatch<_Float16>((const _Float16*)in, gamma, beta, out_t, R, D, s);

@@ -74,6 +74,9 @@ def parse(argv=None):
                          "this process (bit-identical kernels)")
     ap.add_argument("--ab-fold", action="store_true",
                     help="also time a second model with options ln_fold=False in this process (diagnostic)")
+    ap.add_argument("--ab-options", default="",
+                    help="diagnostic: also time a second model with these options "
+                         "('name=0|1,...', e.g. 'resid_f32=1') interleaved in this process")
     return ap.parse_args(argv)
 
 
@@ -361,13 +364,18 @@ def run(args, backend="nccl", load_model=None):
             model.set_gemm_variant(which, 0)
         abg = {k: dict(runs=v, median=statistics.median(v)) for k, v in abg.items()}
     abf = None
-    if args.ab_fold:
-        m0 = load_model(args.model, dev, args.dtype, options={"ln_fold": False})
+    if args.ab_fold or args.ab_options:
+        alt = ({"ln_fold": False} if args.ab_fold else
+               {k: bool(int(v)) for k, v in (p.split("=") for p in args.ab_options.split(","))})
+        m0 = load_model(args.model, dev, args.dtype, options=alt)
         m0.reserve(max(hi - lo, 1), args.classes)
         m0.set_splits(args.splits)
         step0 = make_step(m0)
         step0()
-        abf = {"fold": [], "nofold": [], "fold_flags": model.numerics(), "nofold_flags": m0.numerics()}
+        # "fold" = this run's model, "nofold" = the alternative options (the names
+        # are the --ab-fold ones; `alt_options` says what the alternative was)
+        abf = {"fold": [], "nofold": [], "fold_flags": model.numerics(), "nofold_flags": m0.numerics(),
+               "alt_options": alt}
         for _ in range(3):
             abf["fold"].append(round(n_global * args.steps / timed(step, args.steps), 1))
             abf["nofold"].append(round(n_global * args.steps / timed(step0, args.steps), 1))

@@ -82,9 +82,12 @@ typedef struct miclip_config {
 /* Numerics options of a model handle (miclip_config.options). Every path that
  * changes what the kernels compute is chosen here, explicitly -- the library
  * reads no environment variables.
- * RESID_F32: fp32 residual stream under fp16 compute (default: fp16, the
- *   reference's GPU model). NO_LN_FOLD: run ln_1 / ln_2 as LayerNorm kernels
- *   (default: folded into the QKV / c_fc GEMMs on the fp16 stream).
+ * RESID_F32: fp32 residual stream (default: fp16 under fp16 AND bf16 compute --
+ *   the reference's GPU model keeps its residual stream in half; bf16 compute then
+ *   rounds only the GEMM / attention operands to bf16). NO_LN_FOLD: run ln_1 / ln_2
+ *   as LayerNorm kernels (default under fp16 compute: folded into the QKV / c_fc
+ *   GEMMs on the fp16 stream; bf16 compute never folds: the GEMM would read the fp16
+ *   stream as its bf16 operand).
  * MX_OUT_FP16 (MICLIP_MXFP8): keep the vision out-projection fp16 (default MX-fp8).
  * MX_GELU_ERF (MICLIP_MXFP8): exact-erf GELU in the MX c_fc epilogue (default: the
  *   tanh form, <= 4.8e-4 from erf, below the e4m3 step).

@@ -72,23 +72,32 @@ def test_encode_image_matches_reference(golden, tag, name, dtype):
     report(f"{tag}/{dtype}", feats, g["image"], COS_TOL, COS_TOL)
 
 
-def test_fp32_residual_stream_option(golden):
-    """options={"resid_f32": True} keeps an fp32 residual stream under fp16 compute
-    (the default streams fp16 like the reference's GPU model); both meet the tolerance."""
+@pytest.mark.parametrize("dtype", ["fp16", "bf16"])
+def test_fp32_residual_stream_option(golden, dtype):
+    """options={"resid_f32": True} keeps an fp32 residual stream (the default streams
+    fp16 under fp16 and bf16 compute, like the reference's GPU model); both meet the
+    tolerance, raw and centred, and the text tower follows the same option."""
     import miclip
     from miclip.weights import synthetic_images
     g = golden("vitb16")
     imgs = torch.from_numpy(synthetic_images(g["meta"]["n_images"], 224, seed=0)).cuda()
     _models.clear()
-    _, m32, _ = miclip.load("ViT-B/16", device="cuda", compute_dtype="fp16",
+    _, m32, _ = miclip.load("ViT-B/16", device="cuda", compute_dtype=dtype,
                             options={"resid_f32": True})
     assert not m32.numerics()["resid16"]
     f32 = m32.encode_image(imgs).cpu()
+    t32 = m32.encode_text(torch.from_numpy(g["tokens"]).long().cuda())[1].cpu()
     del m32
-    f16 = _model("ViT-B/16", "fp16").encode_image(imgs).cpu()
-    d32, d16 = _one_minus_cos(f32, g["image"]), _one_minus_cos(f16, g["image"])
-    print(f"vitb16: 1-cos fp32 stream {d32.max():.2e}, fp16 stream {d16.max():.2e}")
-    assert d32.max() <= COS_TOL and d16.max() <= COS_TOL
+    m16 = _model("ViT-B/16", dtype)
+    assert m16.numerics()["resid16"]
+    assert m16.numerics()["lnfold"] == (dtype == "fp16")
+    f16 = m16.encode_image(imgs).cpu()
+    t16 = m16.encode_text(torch.from_numpy(g["tokens"]).long().cuda())[1].cpu()
+    report(f"vitb16/{dtype} fp32 stream", f32, g["image"], COS_TOL, COS_TOL)
+    report(f"vitb16/{dtype} fp16 stream", f16, g["image"], COS_TOL, COS_TOL)
+    dt32, dt16 = _one_minus_cos(t32, g["text_proj"]), _one_minus_cos(t16, g["text_proj"])
+    print(f"vitb16/{dtype}: text 1-cos fp32 stream {dt32.max():.2e}, fp16 stream {dt16.max():.2e}")
+    assert dt32.max() <= COS_TOL and dt16.max() <= COS_TOL
     assert not torch.equal(f32, f16), "the option did not change the stream"
 
 
