@@ -379,8 +379,8 @@ int mx_act(const miclip_model* m, int act) {
 int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, int W, int H,
               int dh, int causal, hipStream_t s, bool cls_only = false) {
   const int M = items * N, dt = m->dtype, r16 = m->resid16;
-  const int vln = M >= 16384 ? m->gemm_variant[0] : 0;
-  const int vres = M >= 16384 ? m->gemm_variant[1] : 0;
+  const int vln = M >= 256 ? m->gemm_variant[0] : 0;
+  const int vres = M >= 256 ? m->gemm_variant[1] : 0;
   const double dM = M, dW = W, rb = r16 ? 2 : 4;  // residual bytes per element
   const bool mx = b.s_qkv != nullptr;   // MX-fp8 operands for QKV / c_fc / c_proj (vision)
   const bool fold = m->lnfold && b.wf_qkv;

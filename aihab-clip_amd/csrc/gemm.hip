@@ -846,8 +846,13 @@ MICLIP_DEV void wait_vmcnt_tile(int n) {
     case 36: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
     case 32: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
     case 28: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
+    case 22: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); break;
+    case 21: asm volatile("s_waitcnt vmcnt(21)" ::: "memory"); break;
     case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
@@ -856,7 +861,7 @@ MICLIP_DEV void wait_vmcnt_tile(int n) {
 // K-tile DMAs of every odd K-tile are skipped (the loop reuses stale LDS), 2 =
 // only K-tiles 0 and 1 are fetched. Used to tell the L2->LDS path from the
 // schedule as the main loop's limit (scripts/bench_ops.py variant suffixes).
-template <typename T, class Epi, bool TRQ = true, int DIAG = 0>
+template <typename T, class Epi, bool TRQ = true, int DIAG = 0, int RB = 4>
 __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
                                                        const T* __restrict__ W, int M, int N,
                                                        int K, Epi epi, int gm, int ntm_dp,
@@ -864,6 +869,15 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
   // transposed accumulators (TrAcc epilogues): MFMA operands swapped, so each
   // lane's accumulator holds 4 consecutive output columns of one output row
   constexpr bool TR = TRQ && TrAcc<Epi>::value;
+  // RB = 16-row blocks per wave quadrant: 4 -> 256-row tiles (the default), 3 ->
+  // 192-row tiles (transposed-accumulator epilogues only; the launcher picks them
+  // where a launch of 256-row tiles would leave CUs idle, e.g. ViT-B/32's N = 768
+  // GEMMs at M = 12 800). Same MFMA chains and epilogue arithmetic per element.
+  static_assert(RB == 4 || (RB == 3 && TR && DIAG == 0), "192-row tiles: TR epilogues only");
+  constexpr int QR = RB * 16;            // rows of one wave quadrant
+  constexpr int SR = 2 * QR;             // rows of one A half-tile slot (both wave rows)
+  constexpr int TM = 2 * SR;             // tile rows
+  constexpr int APC = SR / 8;            // 1-KiB A pieces per slot (16 or 12)
   constexpr int HALF = 128 * 128;        // bytes of one half-tile slot
   constexpr int EPI_LD = 260;            // fp32 row stride of the epilogue staging
   constexpr int STG = 4 * HALF;          // staging: 64 rows in the buffer-1 half onward
@@ -887,24 +901,33 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
   const int wr = wave >> 2, wc = wave & 3;
   const int lchunk = (lane & 7) ^ (lane >> 3);
   const int fr = lane & 15, fk = lane >> 4;
-  const int aoff = (wr * 64 + fr) * 128, boff = (wc * 32 + fr) * 128;
+  const int aoff = (wr * QR + fr) * 128, boff = (wc * 32 + fr) * 128;
   const int sw0 = ((0 + fk) ^ (fr & 7)) << 4, sw1 = ((4 + fk) ^ (fr & 7)) << 4;
   const int ec = (tid & 63) * 4;
 
+  // A pieces of a slot: RB 4: 16 = 2 per wave (pieces 2w, 2w+1); RB 3: 12 = wave w's
+  // piece w and, for waves 0-3 (wave row 0), piece w + 8 -- so a wave's op count per
+  // A stage is a function of its wave row (2 or 1), which the counted waits use
+  auto apiece = [&](int pp) { return RB == 4 ? wave * 2 + pp : wave + 8 * pp; };
+  auto ahas = [&](int pp) { return RB == 4 || pp == 0 || wave < 4; };   // wave-uniform
   // LDS-DMA sources of tile `id` (slot row sr = piece*8 + (lane>>3))
   auto sources = [&](int id, int& m0_, int& n0_, const T* (&as)[2][2], const T* (&bs)[2][2]) {
     int tm_, tn_;
     group_tile(xcd_remap(id, ndp), ntm, ntn, gm, tm_, tn_);
-    m0_ = tm_ * 256;
+    m0_ = tm_ * TM;
     n0_ = tn_ * 256;
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int pp = 0; pp < 2; ++pp) {
-        const int sr = (wave * 2 + pp) * 8 + (lane >> 3);
-        int ar = m0_ + (sr >> 6) * 128 + h * 64 + (sr & 63);
+        // A piece apiece(pp) of slot h: slot rows 0..QR-1 are wave row 0's quadrant
+        // rows h*QR.., QR..SR-1 wave row 1's (tile rows SR + h*QR ..)
+        const int ap = apiece(pp);
+        const int asr = (ap < APC ? ap : 0) * 8 + (lane >> 3);
+        int ar = m0_ + (asr / QR) * SR + h * QR + (asr % QR);
         ar = ar < M ? ar : M - 1;
         as[h][pp] = A + (size_t)ar * K + lchunk * 8;
+        const int sr = (wave * 2 + pp) * 8 + (lane >> 3);
         const int bc = n0_ + (sr >> 5) * 64 + h * 32 + (sr & 31);
         bs[h][pp] = W + (size_t)bc * K + lchunk * 8;
       }
@@ -920,20 +943,26 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
       if (tile >= 2) return;
     }
     const int buf = tile & 1, k0 = tile * 64;
-    char* dst = smem + (buf * 4 + slot_kind) * HALF + wave * 2048;
-    const T* const* src = slot_kind < 2 ? asrc[slot_kind] : bsrc[slot_kind - 2];
-    glds16(src[0] + k0, dst);
-    glds16(src[1] + k0, dst + 1024);
+    char* slot = smem + (buf * 4 + slot_kind) * HALF;
+    if (slot_kind < 2) {
+      const T* const* src = asrc[slot_kind];
+      glds16(src[0] + k0, slot + apiece(0) * 1024);
+      if (ahas(1)) glds16(src[1] + k0, slot + apiece(1) * 1024);
+    } else {
+      const T* const* src = bsrc[slot_kind - 2];
+      glds16(src[0] + k0, slot + wave * 2048);
+      glds16(src[1] + k0, slot + wave * 2048 + 1024);
+    }
   };
 
-  f32x4 acc[2][2][4][2];
-  i16x8 af[2][4], bf[2][2];
+  f32x4 acc[2][2][RB][2];
+  i16x8 af[2][RB], bf[2][2];
   // phase 2 = (A1, B1) finds B1 still in bf from phase 1 (same K-tile buffer):
   // load_b = false there, 28 fragment reads per K-tile instead of 32
   auto quadrant = [&](const char* sa, const char* sb, bool load_a, bool load_b) {
     if (load_a) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < RB; ++i) {
         af[0][i] = *(const i16x8*)(sa + i * 2048 + sw0);
         af[1][i] = *(const i16x8*)(sa + i * 2048 + sw1);
       }
@@ -954,7 +983,7 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < RB; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const f32x4 c = (FIRST && s == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[qi][qj][i][j];
@@ -996,8 +1025,9 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
       if constexpr (IsLN<Epi>::value) {
         if (wave == 1) glds16_hidden(epi.colsum + n0 + lo * 4, tcs);
         const int d = wave * 64 + lo, r = m0 + (d >> 1);
-        glds4_hidden((const float*)(epi.stats + (r < M ? r : M - 1)) + (d & 1),
-                     (const char*)tst + wave * 256);
+        if (RB == 4 || wave < TM / 32)   // TM rows x 2 words, 64 per wave
+          glds4_hidden((const float*)(epi.stats + (r < M ? r : M - 1)) + (d & 1),
+                       (const char*)tst + wave * 256);
       }
     }
     if (prev_stores < 0) {
@@ -1007,12 +1037,15 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
       stage(2, 0);
       stage(0, 1);
       stage(3, 1);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      if (RB == 4 || wr == 0)
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else   // RB 3, wave row 1: one A piece per stage
+        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     } else {
       // K-tile 0 was prefetched during the previous epilogue
       stage(0, 1);
       stage(3, 1);
-      wait_vmcnt_tile(4 + prev_stores);
+      wait_vmcnt_tile((RB == 4 || wr == 0 ? 4 : 3) + prev_stores);
     }
     lds_barrier();
     if (wr == 1) lds_barrier();   // stagger (wave-uniform)
@@ -1035,10 +1068,14 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
         }
         if (p == 3 && wr == 1 && t + 1 < nk) {
           MICLIP_KSTAMP(1);
-          if (t + 2 < nk)
-            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-          else
+          if (t + 2 < nk) {
+            if constexpr (RB == 4)   // A0(t+2) may stay in flight: 2 ops (RB 3: 1)
+              asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            else
+              asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+          } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
           MICLIP_KSTAMP(6);
         }
         const int qi = (p >= 2) ? 1 : 0;
@@ -1085,10 +1122,14 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
         sources(nid, m0, n0, asrc, bsrc);
 #pragma unroll
         for (int kind = 0; kind < 4; ++kind) {
-          const T* const* src = kind < 2 ? asrc[kind] : bsrc[kind - 2];
-          char* dst = smem + kind * HALF + wave * 2048;
-          glds16_hidden(src[0], dst);
-          glds16_hidden(src[1], dst + 1024);
+          char* slot = smem + kind * HALF;
+          if (kind < 2) {
+            glds16_hidden(asrc[kind][0], slot + apiece(0) * 1024);
+            if (ahas(1)) glds16_hidden(asrc[kind][1], slot + apiece(1) * 1024);
+          } else {
+            glds16_hidden(bsrc[kind - 2][0], slot + wave * 2048);
+            glds16_hidden(bsrc[kind - 2][1], slot + wave * 2048 + 1024);
+          }
         }
       }
     };
@@ -1098,7 +1139,7 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
     // loop's compiler-visible LDS-DMA as in flight), and issued here that wait
     // also drained this prefetch -- every tile's epilogue started one DMA round
     // trip late.
-    const bool full = cm0 + 256 <= M;
+    const bool full = cm0 + TM <= M;
     MICLIP_STAMP(2);              // tile boundary: epilogue operands, prefetch issue
     if constexpr (TR) {
       // ---- transposed-accumulator epilogue: 2 passes of 128 rows (qi: tile rows
@@ -1130,23 +1171,25 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
 #pragma unroll
       for (int qi = 0; qi < 2; ++qi) {
         if (qi > 0) lds_barrier();   // pass 0's readers are done with the image
-        float2 ts[4];
+        float2 ts[RB];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < RB; ++i) {
           ts[i] = make_float2(0.f, 0.f);
-          if constexpr (IsLN<Epi>::value) ts[i] = tst[wr * 128 + qi * 64 + i * 16 + fr];
+          if constexpr (IsLN<Epi>::value) ts[i] = tst[wr * SR + qi * QR + i * 16 + fr];
         }
         // fp16 residual stream: the 8 x pieces this lane adds at readback (row
         // R + h of each pair, columns 8li .. 8li+7: 16 B, row-contiguous), loaded
         // now so their latency hides under the staging math (after the LDS reads
         // above: hipcc's vmcnt(0) in front of the epilogue's first LDS read would
         // otherwise wait for them)
-        u32x4 xq[8];
+        // readback rows per wave and pass: SR / 8 (16, or 12 for RB 3)
+        constexpr int RPW = SR / 8;
+        u32x4 xq[RPW / 2];
         if constexpr (PrefetchX<Epi>::value) {
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const int ir = wave * 16 + 2 * k + (lane >> 5);
-            const int row = cm0 + (ir >> 6) * 128 + qi * 64 + (ir & 63);
+          for (int k = 0; k < RPW / 2; ++k) {
+            const int ir = wave * RPW + 2 * k + (lane >> 5);
+            const int row = cm0 + (ir / QR) * SR + qi * QR + (ir % QR);
             xq[k] = *(const u32x4*)(epi.X + (size_t)(row < M ? row : M - 1) * epi.ldx + cn0 +
                                     (lane & 31) * 8);
           }
@@ -1157,8 +1200,8 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
           for (int j = 0; j < 2; ++j) {
             const int c4 = wc * 16 + qj * 8 + j * 4 + fk;   // this lane's column quad
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int ir = wr * 64 + i * 16 + fr;         // image row
+            for (int i = 0; i < RB; ++i) {
+              const int ir = wr * QR + i * 16 + fr;         // image row
               const f32x4 a = acc[qi][qj][i][j];
               const float4 v = make_float4(a[0], a[1], a[2], a[3]);
               i16x4 o;
@@ -1175,7 +1218,7 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
           // retires in issue order)
           if constexpr (PrefetchX<Epi>::value) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(xq[k]));
+            for (int k = 0; k < RPW / 2; ++k) asm volatile("" ::"v"(xq[k]));
           }
           prefetch_next();   // before this pass's stores (prev_stores: EpiStores)
         }
@@ -1191,11 +1234,11 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
         const int h = lane >> 5, li = lane & 31;
         auto* cb = tr_out(epi) + cn0 + li * 8;
 #pragma unroll
-        for (int p0 = 0; p0 < 8; p0 += 2) {
+        for (int p0 = 0; p0 < RPW / 2; p0 += 2) {
           i16x4 va[2], vb[2];
 #pragma unroll
           for (int p = 0; p < 2; ++p) {
-            const int R = wave * 16 + 2 * (p0 + p);
+            const int R = wave * RPW + 2 * (p0 + p);
             va[p] = *(const i16x4*)(img + R * TLD + h * 256 + li * 8);
             vb[p] = *(const i16x4*)(img + (R + 1) * TLD + h * 256 + li * 8);
           }
@@ -1212,8 +1255,8 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
               Epi::template add_x<4>(t, x);
               w = (u32x4){t[0], t[1], t[2], t[3]};
             }
-            const int ir = wave * 16 + 2 * (p0 + p) + h;
-            const int row = cm0 + (ir >> 6) * 128 + qi * 64 + (ir & 63);
+            const int ir = wave * RPW + 2 * (p0 + p) + h;
+            const int row = cm0 + (ir / QR) * SR + qi * QR + (ir % QR);
             if (full || row < M) *(u32x4*)(cb + (size_t)row * tr_ld(epi)) = w;
           }
         }
@@ -1337,16 +1380,17 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
     }
     }
     lds_barrier();                 // staging (buffer-1 half) free for the next tile
-    prev_stores = full ? EpiStores<Epi, TR>::n : 0;
+    // RB 3: 12 rows per wave and pass instead of 16 (TR epilogues only)
+    prev_stores = full ? EpiStores<Epi, TR>::n * RB / 4 : 0;
     MICLIP_STAMP(3);              // epilogue
   }
   // the row tail on the same workgroups
   for (int task = blockIdx.x; task < ntail; task += gridDim.x) {
     lds_barrier();
     if (tail_wide)
-      gemm_tail_wg<T, Epi, 2, 128>(A, W, M, N, K, epi, ntm * 256, task, smem);
+      gemm_tail_wg<T, Epi, 2, 128>(A, W, M, N, K, epi, ntm * TM, task, smem);
     else
-      gemm_tail_wg<T, Epi, 1, 64>(A, W, M, N, K, epi, ntm * 256, task, smem);
+      gemm_tail_wg<T, Epi, 1, 64>(A, W, M, N, K, epi, ntm * TM, task, smem);
   }
   MICLIP_STAMP(4);                // row tail
   MICLIP_STAMP_END(blockIdx.x * 8 + wave);
@@ -2585,6 +2629,7 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   const bool env_variant = false;   // an explicit variant never falls back silently
   if (variant != 0 && variant != 128 && variant != 256 && variant != 257 && variant != 258 &&
       variant != 259 && variant != 260 && variant != 2 && variant != 3 && variant != 300 &&
+      variant != 192 &&
       !(variant >= 400 && variant < 420) && variant != 508 && variant != 516 &&
       !(variant >= 530 && variant <= 534))
     return hipErrorInvalidValue;
@@ -2694,9 +2739,29 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   // c_fc +1 %, c_proj +1 %)
   // (from half a round of 256x256 tiles up: ViT-B/32 bs=128 QKV 225 tiles 0.047 ->
   // 0.028 ms, out-proj bs=256 150 tiles 0.051 -> 0.028 ms vs the 128x128 kernel)
+  const bool by_size = variant == 0;   // the launcher picks (not an explicit A/B variant)
   if (variant == 0 && !IsPatch<Epi>::value && N % 256 == 0 && K >= 128 &&
       2 * ((M + 255) / 256) * (N / 256) >= cu_count())
     variant = 259;
+  // 192-row tiles (gemm256s_kernel RB 3, transposed-accumulator epilogues): where a
+  // launch of 256-row tiles is a single partial round and 192-row tiles still fit
+  // one round, every CU that works does 3/4 of a tile's MFMAs and epilogue bytes
+  // (ViT-B/32 bs=256 out-proj / c_proj: 150 -> 201 tiles on 256 CUs). Variant 192
+  // forces them (tests, A/B).
+  if constexpr (TrAcc<Epi>::value && !IsPatch<Epi>::value) {
+    if ((variant == 259 || variant == 192) && N % 256 == 0 && K >= 128 && !variant_tracc_off &&
+        !diag) {
+      const int ncu = cu_count(), ntm3 = (M + 191) / 192, t192 = ntm3 * (N / 256);
+      const int t256 = ((M + 255) / 256) * (N / 256);
+      if (variant == 192 || (by_size && t256 <= ncu && t192 <= ncu)) {
+        hipLaunchKernelGGL((gemm256s_kernel<T, Epi, true, 0, 3>), dim3(t192 < ncu ? t192 : ncu),
+                           dim3(512), 0, s, (const T*)A, (const T*)W, M, N, K, epi, gm, ntm3, 0,
+                           0);
+        return hipGetLastError();
+      }
+    }
+  }
+  if (variant == 192) return hipErrorInvalidValue;   // not a transposed-accumulator epilogue
   if (variant == 259 && !IsPatch<Epi>::value && N % 256 == 0 && K >= 128) {
     // persistent staggered kernel, LDS-staged epilogue + next-tile prefetch
     const TailPlan tp = notail ? TailPlan{(M + 255) / 256, 0, 0} : plan_tail(M, N);

@@ -250,7 +250,7 @@ int64_t miclip_model_bytes(const miclip_model* m);
 #define MICLIP_MODEL_MX_OUT 16
 #define MICLIP_MODEL_MX_GELU_TANH 32
 int miclip_model_flags(const miclip_model* m);
-/* Diagnostics: the GEMM kernel of the full-batch launches (>= 16384 rows) --
+/* Diagnostics: the GEMM kernel of the block launches (>= 256 rows) --
  * which 0: the folded-LN store GEMMs (QKV, c_fc), 1: the fp16 residual GEMMs
  * (out-proj, c_proj); variant 0 (default) / 259 (the 8-wave persistent kernel) /
  * 508, 516 (the 4-wave gemm4s kernel); which 2: the MX-fp8 GEMMs (variants of
