@@ -126,7 +126,7 @@ MICLIP_DEV float half_sum(float x) {
 // re-loaded (4 x 16 B per lane per 256 columns) for every row pair.
 constexpr int kLnRows = 32;
 
-template <int NI, typename T, bool MX>
+template <int NI, typename T, bool MX, int ROWS = kLnRows>
 __global__ __launch_bounds__(256) void layernorm_h2_kernel(const _Float16* in,  // may alias out
                                                            const float* __restrict__ gamma,
                                                            const float* __restrict__ beta,
@@ -141,7 +141,7 @@ __global__ __launch_bounds__(256) void layernorm_h2_kernel(const _Float16* in,  
   __syncthreads();
   const int lane = threadIdx.x & 63, hl = lane & 31;
   const int wave = threadIdx.x >> 6;
-  constexpr int PAIRS = kLnRows / 8;   // row pairs per wave
+  constexpr int PAIRS = ROWS / 8;      // row pairs per wave
   for (int it = 0; it < PAIRS; ++it) {
     const int p2 = ((blockIdx.x * 4 + wave) * PAIRS + it) * 2;   // first row of the pair
     if (p2 >= R) break;                                          // wave-uniform
@@ -304,14 +304,23 @@ __global__ __launch_bounds__(256) void ln_fold_kernel(const T* __restrict__ W,
   }
 }
 
+// Rows per workgroup: 32 (gamma / beta staged once for 32 rows) while that still
+// gives every CU a few workgroups; 8 for smaller launches, where 32-row workgroups
+// leave ~6 waves per CU and the row loads' latency shows (ViT-B/32 bs=256: 12 800
+// rows = 400 workgroups of 32). The arithmetic per row is the same.
 template <typename T, bool MX = false>
 hipError_t ln_h2_dispatch(const _Float16* in, const float* g, const float* b, void* out, int R,
                           int D, hipStream_t s, void* oq = nullptr, void* os = nullptr) {
-  const dim3 grid((R + kLnRows - 1) / kLnRows), block(256);
-#define MICLIP_LNH_CASE(V)                                                                     \
-  case V:                                                                                      \
-    hipLaunchKernelGGL((layernorm_h2_kernel<V, T, MX>), grid, block, 0, s, in, g, b, (T*)out, \
-                       R, D, (uint8_t*)oq, (uint8_t*)os);                                      \
+  const bool small = (R + kLnRows - 1) / kLnRows < 1024;
+  const dim3 grid(small ? (R + 7) / 8 : (R + kLnRows - 1) / kLnRows), block(256);
+#define MICLIP_LNH_CASE(V)                                                                      \
+  case V:                                                                                       \
+    if (small)                                                                                  \
+      hipLaunchKernelGGL((layernorm_h2_kernel<V, T, MX, 8>), grid, block, 0, s, in, g, b,       \
+                         (T*)out, R, D, (uint8_t*)oq, (uint8_t*)os);                            \
+    else                                                                                        \
+      hipLaunchKernelGGL((layernorm_h2_kernel<V, T, MX>), grid, block, 0, s, in, g, b, (T*)out, \
+                         R, D, (uint8_t*)oq, (uint8_t*)os);                                     \
     break;
   switch (D / 256) {
     MICLIP_LNH_CASE(1)
