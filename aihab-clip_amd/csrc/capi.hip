@@ -376,6 +376,15 @@ int mx_act(const miclip_model* m, int act) {
   return act == ACT_GELU && !m->mx_gelu_erf ? ACT_GELU_TANH : act;
 }
 
+// Split count of a CLS-row GEMM (M = images) reducing K: slices of >= 256 k, at most
+// 16, dividing K into whole 64-k steps. A function of K only, so a row's result
+// never depends on the batch.
+int cls_splitk(int K) {
+  int sk = K / 256 < 16 ? K / 256 : 16;
+  while (sk > 1 && K % (sk * 64)) --sk;
+  return sk < 1 ? 1 : sk;
+}
+
 int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, int W, int H,
               int dh, int causal, hipStream_t s, bool cls_only = false) {
   const int M = items * N, dt = m->dtype, r16 = m->resid16;
@@ -415,12 +424,19 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
                 dM * 2 * dW * 2 + 10 * dW * dW * 2);
     MICLIP_HIP(attention_q0(dt, w.qkv, w.o, items, N, H, s, dh));
     MICLIP_HIP(gather_rows(w.x, w.xc, items, N, W, r16 ? 2 : 4, s));
+    // the GEMMs below have M = images: split K through an fp32 workspace in the
+    // QKV buffer (free after attention_q0; sk * items * 4W floats fit in its
+    // items * N * 3W elements for N >= 43 tokens)
+    float* skws = (float*)w.qkv;
+    const bool sk_ok = (size_t)16 * 4 * W * 4 <= (size_t)N * 3 * W * elt();
+    const int sk1 = sk_ok ? cls_splitk(W) : 1, sk4 = sk_ok ? cls_splitk(4 * W) : 1;
     if (b.s_out) {   // MX-fp8 out-proj (vision tower of an MX model)
       MICLIP_HIP(quant_mx(1, w.o, items, W, w.hq, w.hs, s));
       MICLIP_HIP(gemm_mx(w.hq, w.hs, b.w_out, b.s_out, b.b_out, w.xc, nullptr, items, W, W, 1,
                          ACT_NONE, s, m->gemm_variant[2]));
     } else {
-      MICLIP_HIP(gemm_residual(dt, w.o, b.w_out, b.b_out, w.xc, items, W, W, s, 0, r16));
+      MICLIP_HIP(gemm_residual(dt, w.o, b.w_out, b.b_out, w.xc, items, W, W, s, 0, r16, skws,
+                               sk1));
     }
     if (mx) {   // MX-fp8 MLP on the CLS rows (their scale blocks are row-local)
       MICLIP_HIP(layernorm(dt, w.xc, nullptr, 1, b.ln2_g, b.ln2_b, nullptr, nullptr, items, W, 0,
@@ -434,13 +450,15 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
     if (fold) {
       MICLIP_HIP(ln_stats(w.xc, w.stats, items, W, s, b.fs_fc));
       MICLIP_HIP(gemm_store_ln(dt, w.xc, b.wf_fc, b.c_fc, b.cs_fc, w.stats, w.f, items, 4 * W, W,
-                               m->cfg.act, s));
+                               m->cfg.act, s, 0, skws, sk1));
     } else {
       MICLIP_HIP(
           layernorm(dt, w.xc, nullptr, 1, b.ln2_g, b.ln2_b, nullptr, w.h, items, W, 0, s, r16));
-      MICLIP_HIP(gemm_store(dt, w.h, b.w_fc, b.b_fc, w.f, items, 4 * W, W, m->cfg.act, s));
+      MICLIP_HIP(gemm_store(dt, w.h, b.w_fc, b.b_fc, w.f, items, 4 * W, W, m->cfg.act, s, 0, skws,
+                            sk1));
     }
-    MICLIP_HIP(gemm_residual(dt, w.f, b.w_proj, b.b_proj, w.xc, items, W, 4 * W, s, 0, r16));
+    MICLIP_HIP(gemm_residual(dt, w.f, b.w_proj, b.b_proj, w.xc, items, W, 4 * W, s, 0, r16, skws,
+                             sk4));
     return 0;
   }
   {

@@ -47,10 +47,11 @@ namespace {
 
 constexpr int BK = 64;
 
+// ldk: row stride of A and W (elements); K: the k extent this workgroup reduces
+// (ldk = K, except for the split-K partials below). bid: the tile (pre-remap).
 template <typename T, int BM, int BN, class Epi>
-__global__ __launch_bounds__(256) void gemm_nt_kernel(const T* __restrict__ A,
-                                                      const T* __restrict__ W, int M, int N,
-                                                      int K, Epi epi) {
+MICLIP_DEV void gemm_nt_body(const T* __restrict__ A, const T* __restrict__ W, int M, int N,
+                             int K, int ldk, Epi epi, int bid0) {
   constexpr int WN = 2;
   constexpr int TM = BM / 2, TN = BN / WN;
   constexpr int FM = TM / 16, FN = TN / 16;
@@ -63,7 +64,7 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const T* __restrict__ A,
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int ntn = N / BN, ntm = (M + BM - 1) / BM;
-  const int bid = xcd_remap(blockIdx.x, ntm * ntn);
+  const int bid = xcd_remap(bid0, ntm * ntn);
   const int tm = bid / ntn, tn = bid - tm * ntn;
   const int m0 = tm * BM, n0 = tn * BN;
 
@@ -76,12 +77,12 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const T* __restrict__ A,
   for (int p = 0; p < APW; ++p) {
     int row = m0 + (wave * APW + p) * 8 + prow;
     row = row < M ? row : M - 1;
-    a_src[p] = A + (size_t)row * K + lchunk * 8;
+    a_src[p] = A + (size_t)row * ldk + lchunk * 8;
   }
 #pragma unroll
   for (int p = 0; p < BPW; ++p) {
     const int row = n0 + (wave * BPW + p) * 8 + prow;
-    b_src[p] = W + (size_t)row * K + lchunk * 8;
+    b_src[p] = W + (size_t)row * ldk + lchunk * 8;
   }
 
   // fragment read offsets (bytes within a stage)
@@ -151,6 +152,45 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const T* __restrict__ A,
       }
     }
   }
+}
+
+template <typename T, int BM, int BN, class Epi>
+__global__ __launch_bounds__(256) void gemm_nt_kernel(const T* __restrict__ A,
+                                                      const T* __restrict__ W, int M, int N,
+                                                      int K, Epi epi) {
+  gemm_nt_body<T, BM, BN>(A, W, M, N, K, K, epi, blockIdx.x);
+}
+
+// Split-K for the small-M GEMMs of the CLS-only last block (M = images, K up to
+// 4W: a few 128x128 tiles would each walk the whole K alone). Split s =
+// blockIdx.y reduces k in [s*Ks, (s+1)*Ks) into an fp32 partial plane ws[s][M][N];
+// splitk_reduce_kernel sums the S planes in ascending s (fixed order: deterministic,
+// and the same for every M, so a row's result does not depend on the batch) and
+// applies the epilogue's own put4 (bias, activation, folded LN, fp16 residual).
+template <typename T>
+__global__ __launch_bounds__(256) void gemm_nt_splitk_kernel(const T* __restrict__ A,
+                                                             const T* __restrict__ W, int M,
+                                                             int N, int K, int Ks,
+                                                             float* __restrict__ ws) {
+  const int sk = blockIdx.y;
+  gemm_nt_body<T, 128, 128>(A + (size_t)sk * Ks, W + (size_t)sk * Ks, M, N, Ks, K,
+                            EpiF32{ws + (size_t)sk * M * N, nullptr, N}, blockIdx.x);
+}
+
+template <class Epi>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int S,
+                                                            int M, int N, Epi epi) {
+  const int64_t i4 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int n4 = N / 4;
+  if (i4 >= (int64_t)M * n4) return;
+  const int r = (int)(i4 / n4), c = (int)(i4 - (int64_t)r * n4) * 4;
+  const size_t plane = (size_t)M * N, off = (size_t)r * N + c;
+  float4 v = *(const float4*)(ws + off);
+  for (int s = 1; s < S; ++s) {
+    const float4 u = *(const float4*)(ws + s * plane + off);
+    v = make_float4(v.x + u.x, v.y + u.y, v.z + u.z, v.w + u.w);
+  }
+  epi.put4(r, c, v, epi.bias4(c));
 }
 
 
@@ -2615,8 +2655,18 @@ bool gemm_shape_ok(int M, int N, int K) {
 
 template <typename T, class Epi>
 hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hipStream_t s,
-                  int variant = 0) {
+                  int variant = 0, float* skws = nullptr, int sk = 1) {
   if (!gemm_shape_ok(M, N, K)) return hipErrorInvalidValue;
+  if (sk > 1) {   // split-K (small M, long K: the CLS-only last block), deterministic
+    if (!skws || K % (sk * BK) || N % 128) return hipErrorInvalidValue;
+    const int tiles = ((M + 127) / 128) * (N / 128);
+    hipLaunchKernelGGL((gemm_nt_splitk_kernel<T>), dim3(tiles, sk), dim3(256), 0, s,
+                       (const T*)A, (const T*)W, M, N, K, K / sk, skws);
+    const int64_t n4 = (int64_t)M * (N / 4);
+    hipLaunchKernelGGL((splitk_reduce_kernel<Epi>), dim3((unsigned)((n4 + 255) / 256)), dim3(256),
+                       0, s, (const float*)skws, sk, M, N, epi);
+    return hipGetLastError();
+  }
   const bool notail = variant & kGemmNoTail;
   const bool tail_first = variant & kGemmTailFirst;
   const bool stagger = variant & kGemmStagger;
@@ -2857,39 +2907,39 @@ constexpr int gemm_nt() { return 0; }
 
 template <typename T>
 hipError_t gemm_store_t(const void* A, const void* W, const float* bias, void* C, int M, int N,
-                        int K, int act, hipStream_t s, int v) {
+                        int K, int act, hipStream_t s, int v, float* skws, int sk) {
   const int nt = gemm_nt();
   switch (act) {
     case ACT_NONE:
-      return launch<T>(A, W, M, N, K, EpiStore<T, ACT_NONE>{(T*)C, bias, N, nt}, s, v);
+      return launch<T>(A, W, M, N, K, EpiStore<T, ACT_NONE>{(T*)C, bias, N, nt}, s, v, skws, sk);
     case ACT_QUICKGELU:
-      return launch<T>(A, W, M, N, K, EpiStore<T, ACT_QUICKGELU>{(T*)C, bias, N, nt}, s, v);
+      return launch<T>(A, W, M, N, K, EpiStore<T, ACT_QUICKGELU>{(T*)C, bias, N, nt}, s, v, skws, sk);
     case ACT_GELU:
-      return launch<T>(A, W, M, N, K, EpiStore<T, ACT_GELU>{(T*)C, bias, N, nt}, s, v);
+      return launch<T>(A, W, M, N, K, EpiStore<T, ACT_GELU>{(T*)C, bias, N, nt}, s, v, skws, sk);
     default:
       return hipErrorInvalidValue;
   }
 }
 
 hipError_t gemm_store(int dtype, const void* A, const void* W, const float* bias, void* C, int M,
-                      int N, int K, int act, hipStream_t s, int v) {
-  if (dtype == kF16) return gemm_store_t<_Float16>(A, W, bias, C, M, N, K, act, s, v);
-  return gemm_store_t<__bf16>(A, W, bias, C, M, N, K, act, s, v);
+                      int N, int K, int act, hipStream_t s, int v, float* skws, int sk) {
+  if (dtype == kF16) return gemm_store_t<_Float16>(A, W, bias, C, M, N, K, act, s, v, skws, sk);
+  return gemm_store_t<__bf16>(A, W, bias, C, M, N, K, act, s, v, skws, sk);
 }
 
 template <typename T>
 hipError_t gemm_store_ln_t(const void* A, const void* W, const float* c, const float* colsum,
                            const void* stats, void* C, int M, int N, int K, int act,
-                           hipStream_t s, int v) {
+                           hipStream_t s, int v, float* skws, int sk) {
   const float2* st = (const float2*)stats;
   switch (act) {
     case ACT_NONE:
-      return launch<T>(A, W, M, N, K, EpiStoreLN<T, ACT_NONE>{(T*)C, c, colsum, st, N}, s, v);
+      return launch<T>(A, W, M, N, K, EpiStoreLN<T, ACT_NONE>{(T*)C, c, colsum, st, N}, s, v, skws, sk);
     case ACT_QUICKGELU:
       return launch<T>(A, W, M, N, K, EpiStoreLN<T, ACT_QUICKGELU>{(T*)C, c, colsum, st, N}, s,
-                       v);
+                       v, skws, sk);
     case ACT_GELU:
-      return launch<T>(A, W, M, N, K, EpiStoreLN<T, ACT_GELU>{(T*)C, c, colsum, st, N}, s, v);
+      return launch<T>(A, W, M, N, K, EpiStoreLN<T, ACT_GELU>{(T*)C, c, colsum, st, N}, s, v, skws, sk);
     default:
       return hipErrorInvalidValue;
   }
@@ -2897,22 +2947,27 @@ hipError_t gemm_store_ln_t(const void* A, const void* W, const float* c, const f
 
 hipError_t gemm_store_ln(int dtype, const void* A, const void* W, const float* c,
                          const float* colsum, const void* stats, void* C, int M, int N, int K,
-                         int act, hipStream_t s, int v) {
+                         int act, hipStream_t s, int v, float* skws, int sk) {
   if (!c || !colsum || !stats) return hipErrorInvalidValue;
-  if (dtype == kF16) return gemm_store_ln_t<_Float16>(A, W, c, colsum, stats, C, M, N, K, act, s, v);
-  return gemm_store_ln_t<__bf16>(A, W, c, colsum, stats, C, M, N, K, act, s, v);
+  if (dtype == kF16)
+    return gemm_store_ln_t<_Float16>(A, W, c, colsum, stats, C, M, N, K, act, s, v, skws, sk);
+  return gemm_store_ln_t<__bf16>(A, W, c, colsum, stats, C, M, N, K, act, s, v, skws, sk);
 }
 
 hipError_t gemm_residual(int dtype, const void* A, const void* W, const float* bias, void* X,
-                         int M, int N, int K, hipStream_t s, int v, int resid16) {
+                         int M, int N, int K, hipStream_t s, int v, int resid16, float* skws,
+                         int sk) {
   if (resid16) {  // fp16 residual stream (fp16 or bf16 operands)
     if (dtype == kBF16)
-      return launch<__bf16>(A, W, M, N, K, EpiResidual<_Float16>{(_Float16*)X, bias, N}, s, v);
-    return launch<_Float16>(A, W, M, N, K, EpiResidual<_Float16>{(_Float16*)X, bias, N}, s, v);
+      return launch<__bf16>(A, W, M, N, K, EpiResidual<_Float16>{(_Float16*)X, bias, N}, s, v,
+                            skws, sk);
+    return launch<_Float16>(A, W, M, N, K, EpiResidual<_Float16>{(_Float16*)X, bias, N}, s, v,
+                            skws, sk);
   }
   if (dtype == kF16)
-    return launch<_Float16>(A, W, M, N, K, EpiResidual<float>{(float*)X, bias, N}, s, v);
-  return launch<__bf16>(A, W, M, N, K, EpiResidual<float>{(float*)X, bias, N}, s, v);
+    return launch<_Float16>(A, W, M, N, K, EpiResidual<float>{(float*)X, bias, N}, s, v, skws,
+                            sk);
+  return launch<__bf16>(A, W, M, N, K, EpiResidual<float>{(float*)X, bias, N}, s, v, skws, sk);
 }
 
 hipError_t gemm_f32(int dtype, const void* A, const void* W, const float* bias, float* C, int M,

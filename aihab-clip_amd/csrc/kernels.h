@@ -18,18 +18,23 @@ enum Act { ACT_NONE = 0, ACT_QUICKGELU = 1, ACT_GELU = 2, ACT_GELU_TANH = 3 };
 // Shapes: N % 128 == 0, K % 64 == 0, any M >= 1; A, W rows K-contiguous.
 // Store epilogue: C (compute dtype, ld = N) = act(acc + bias).
 // `variant`: 0 = pick by size, 128 / 256 = force that tile (tests, A/B timing).
+// skws / sk (the GEMMs of the CLS-only last block): split K into sk deterministic
+// slices through an fp32 workspace skws of sk * M * N floats (K % (64 sk) == 0)
 hipError_t gemm_store(int dtype, const void* A, const void* W, const float* bias, void* C,
-                      int M, int N, int K, int act, hipStream_t s, int variant = 0);
+                      int M, int N, int K, int act, hipStream_t s, int variant = 0,
+                      float* skws = nullptr, int sk = 1);
 // LayerNorm folded into the GEMM (epilogue.h, EpiStoreLN): A = the un-normalised
 // rows, W = W diag(gamma) (ln_fold), stats [M] float2 {mean, rstd} (ln_stats);
 // C = act(rstd * (acc - mean * colsum) + c).
 hipError_t gemm_store_ln(int dtype, const void* A, const void* W, const float* c,
                          const float* colsum, const void* stats, void* C, int M, int N, int K,
-                         int act, hipStream_t s, int variant = 0);
+                         int act, hipStream_t s, int variant = 0, float* skws = nullptr,
+                         int sk = 1);
 // Residual epilogue: X (ld = N) += acc + bias; X fp32, or fp16 when resid16
 // (fp16 compute only: the reference's fp16 GPU residual stream).
 hipError_t gemm_residual(int dtype, const void* A, const void* W, const float* bias, void* X,
-                         int M, int N, int K, hipStream_t s, int variant = 0, int resid16 = 0);
+                         int M, int N, int K, hipStream_t s, int variant = 0, int resid16 = 0,
+                         float* skws = nullptr, int sk = 1);
 // Float epilogue: C (fp32, ld = N) = acc + bias (bias may be null).
 hipError_t gemm_f32(int dtype, const void* A, const void* W, const float* bias, float* C,
                     int M, int N, int K, hipStream_t s, int variant = 0);
