@@ -447,6 +447,104 @@ __global__ __launch_bounds__(DH == 64 ? 640 : 576) void attention_kernel(
   }
 }
 
+MICLIP_DEV void wait_vm_upto(int n) {   // s_waitcnt vmcnt(n), n a small run-time count
+  switch (n) {
+#define MICLIP_VMU(k) \
+  case k:           \
+    asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    MICLIP_VMU(1) MICLIP_VMU(2) MICLIP_VMU(3) MICLIP_VMU(4) MICLIP_VMU(5) MICLIP_VMU(6)
+    MICLIP_VMU(7) MICLIP_VMU(8) MICLIP_VMU(9) MICLIP_VMU(10) MICLIP_VMU(11) MICLIP_VMU(12)
+#undef MICLIP_VMU
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// Head dim 80 (open_clip ViT-H/14, C5), default. attention_kernel<80> holds 110 KiB
+// of K/V, so it runs one workgroup per CU and waits for a head's whole fetch before
+// any MFMA. Here Q goes to LDS by DMA too (an unpadded 160-B-row image, 45 KiB at
+// N = 257; its ds_read_b128 Q fragments are conflict-free at that pitch) and the
+// fetch runs in two phases: Q + key tiles 0-3 of K and V, then the rest. Each wave
+// waits only for its own phase-A pieces (vmcnt = its phase-B count), the workgroup
+// syncs, and every wave runs its query chunk over key tiles 0-3 while phase B lands;
+// then a full wait + barrier and tiles 4.. (attend_chunk continuing the online
+// softmax). Same data (padding rows repeat row N - 1), same per-tile arithmetic in
+// the same order as attention_kernel: bit-identical. One chunk per wave.
+template <typename T>
+__global__ __launch_bounds__(576) void attention80s_kernel(const T* __restrict__ qkv,
+                                                           T* __restrict__ out, int N, int H,
+                                                           int Npad, int nchunks, float qk_scale,
+                                                           int prio) {
+  using G = HeadGeom<80>;
+  constexpr int QROWB = 160;   // Q image row: dims 0-79
+  constexpr int TA = 4;        // key tiles in phase A
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  char* kimg = smem;
+  char* vimg = smem + Npad * G::ROWB;
+  char* qimg = smem + 2 * Npad * G::ROWB;
+  const int bh = blockIdx.x;
+  const int b = bh / H, h = bh - b * H;
+  const int D = H * 80, ld = 3 * D;
+  const T* base = qkv + (size_t)b * N * ld + h * 80;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int kvp = Npad * G::ROWB / 1024;   // 1-KiB pieces per K (or V) image
+  const int kva = TA * G::TILEB / 1024;    // ... of which phase A
+  const int qp = Npad * QROWB / 1024;      // Q pieces (Npad % 32 == 0: whole pieces)
+  // attention_kernel<80>'s K / V staging of one piece (192-B rows, swizzled chunks)
+  auto kv_piece = [&](bool isv, int piece) {
+    const int off = piece * 1024 + lane * 16;
+    const int row = off / G::ROWB, pch = (off - row * G::ROWB) >> 4;
+    int c = G::swz(pch, isv ? ((row & 3) << 1) : ((row >> 1) & 7));
+    const T* src;
+    if (isv && c == 80 / 8) {
+      src = (const T*)(std::is_same_v<T, _Float16> ? kOnesF16 : kOnesBF16);
+    } else {
+      if (c * 8 >= 80) c -= 8;
+      const int r = row < N ? row : N - 1;
+      src = base + (size_t)r * ld + (isv ? 2 * D : D) + c * 8;
+    }
+    glds16_hidden(src, (isv ? vimg : kimg) + piece * 1024);
+  };
+  auto q_piece = [&](int piece) {   // padding queries: row N - 1, as load_q
+    const int off = piece * 1024 + lane * 16;
+    const int row = off / QROWB, ch = (off - row * QROWB) >> 4;
+    const int r = row < N ? row : N - 1;
+    glds16_hidden(base + (size_t)r * ld + ch * 8, qimg + piece * 1024);
+  };
+  const int nA = qp + 2 * kva, nB = 2 * (kvp - kva), half = kvp - kva;
+  for (int pc = wave; pc < nA; pc += nw) {
+    if (pc < qp) {
+      q_piece(pc);
+    } else {
+      const int i = pc - qp;
+      kv_piece(i >= kva, i >= kva ? i - kva : i);
+    }
+  }
+  for (int pc = wave; pc < nB; pc += nw) kv_piece(pc >= half, kva + (pc >= half ? pc - half : pc));
+  wait_vm_upto(wave < nB ? (nB - wave + nw - 1) / nw : 0);   // this wave's phase A landed
+  __syncthreads();
+
+  const float c2 = qk_scale * kLog2e;
+  const int chunk = wave;
+  f32x16 o[G::NDT];
+  float lsum = 0.f, m = 0.f;
+  i16x8 qf[G::NKS];
+  const int l32 = lane & 31, hh = lane >> 5;
+  if (chunk < nchunks) {
+    const char* qrow = qimg + (chunk * 32 + l32) * QROWB + hh * 16;
+#pragma unroll
+    for (int s2 = 0; s2 < G::NKS; ++s2) qf[s2] = *(const i16x8*)(qrow + 32 * s2);
+    attend_chunk<T, false, 80>(kimg, vimg, qf, chunk, N, Npad, c2, lane, o, lsum, m, 0, TA, prio,
+                               true, false);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (chunk < nchunks) {
+    attend_chunk<T, false, 80>(kimg, vimg, qf, chunk, N, Npad, c2, lane, o, lsum, m, TA, -1, prio,
+                               false, true);
+    attend_store<T, 80>(o, lsum, chunk, N, out + (size_t)b * N * D + h * 80, D, lane);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Pipelined form: one workgroup walks hpw consecutive (image, head) pairs.
 // While head j is computed, head j+1's K and V are LDS-DMA'd
@@ -1190,7 +1288,28 @@ hipError_t attn_launch_plain(const void* qkv, void* out, int B, int N, int H, hi
 template <typename T, bool CAUSAL>
 hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, hipStream_t s,
                        int variant) {
-  if (dh == 80) return attn_launch_plain<T, CAUSAL, 80>(qkv, out, B, N, H, s);
+  if (dh == 80) {
+    // the two-phase kernel (default) where a chunk per wave fits 9 waves and Q's
+    // image fits beside K / V; variant 1 = attention_kernel<80>
+    const int Npad = (N + 31) & ~31, nchunks = Npad / 32;
+    const size_t lds80 = (size_t)Npad * (2 * HeadGeom<80>::ROWB + 160);
+    if (!CAUSAL && variant != 1 && nchunks <= 9 && Npad >= 160 && lds80 <= 160 * 1024) {
+      static bool a80 = false;
+      if (!a80) {
+        const hipError_t e = hipFuncSetAttribute((const void*)attention80s_kernel<T>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 160 * 1024);
+        if (e != hipSuccess) return e;
+        a80 = true;
+      }
+      hipLaunchKernelGGL((attention80s_kernel<T>), dim3(B * H), dim3(nchunks * 64), lds80, s,
+                         (const T*)qkv, (T*)out, N, H, Npad, nchunks, 1.0f / sqrtf(80.f),
+                         attn_prio());
+      return hipGetLastError();
+    }
+    if (variant == 2) return hipErrorInvalidValue;   // the two-phase kernel does not apply
+    return attn_launch_plain<T, CAUSAL, 80>(qkv, out, B, N, H, s);
+  }
   if (dh != 64) return hipErrorInvalidValue;
   const int Npad = (N + 31) & ~31;
   const int nchunks = Npad / 32;

@@ -107,7 +107,7 @@ def main():
         avs = (8, 9, 8, 9, 8, 9, 2) if 257 <= args.tokens <= 259 else (0, 1, 0, 1)
         if args.attn_variants:
             avs = tuple(int(v) for v in args.attn_variants.split(","))
-        for av in (avs if dh == 64 else (0, 0)):
+        for av in (avs if dh == 64 or args.attn_variants else (0, 0)):
             def fa():
                 rc = lib.miclip_op_attention(0, qkv.data_ptr(), o.data_ptr(), args.batch, args.tokens, H, dh,
                                              0, av, s)

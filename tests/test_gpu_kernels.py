@@ -366,6 +366,31 @@ def test_attention_dh80(lib, dt, B, N, H, causal):
 
 
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
+@pytest.mark.parametrize("B,N,H", [(2, 257, 16), (3, 160, 4), (1, 288, 2), (4, 200, 3), (64, 257, 16)])
+def test_attention_dh80_two_phase_bitexact(lib, dt, B, N, H):
+    """The two-phase head-dim-80 kernel (default, variant 2: Q by LDS-DMA, key tiles 0-3
+    computed while the rest lands) equals attention_kernel<80> (variant 1) bit for bit;
+    outside its range (N < 129 or > 288, causal) variant 2 is refused, not replaced."""
+    code, tdt = DT[dt]
+    g = torch.Generator(device="cuda").manual_seed(B * 1000 + N + H + 801)
+    qkv = (torch.randn(B * N, 3 * H * 80, device="cuda", generator=g) * 1.5).to(tdt)
+    outs = []
+    for v in (1, 2, 0):
+        out = torch.full((B * N + 1, H * 80), 7.0, device="cuda", dtype=tdt)
+        _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), out.data_ptr(), B, N, H, 80, 0,
+                                            v, _stream()))
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+    assert bool((outs[1][B * N] == 7.0).all())
+    for bad_n, causal in ((100, 0), (300, 0), (257, 1)):
+        x = torch.zeros(bad_n, 3 * 80, device="cuda", dtype=tdt)
+        y = torch.zeros(bad_n, 80, device="cuda", dtype=tdt)
+        assert lib.miclip_op_attention(code, x.data_ptr(), y.data_ptr(), 1, bad_n, 1, 80, causal, 2,
+                                       _stream()) != 0
+
+
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
 @pytest.mark.parametrize("B,N,H,dh", [(3, 257, 16, 64), (2, 577, 16, 64), (5, 50, 12, 64),
                                       (2, 257, 16, 80), (1, 1, 1, 64), (2, 640, 2, 64), (1, 768, 2, 80),
                                       (7, 197, 3, 64), (1, 65, 5, 80)])
