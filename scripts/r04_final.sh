@@ -7,7 +7,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp MICLIP_QUIET=1
-O=gpurun_out/r04final
+O=gpurun_out/${OUT:-r04final}
 mkdir -p $O/configs
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 \
   && tail -1 $O/pytest_gpu.log \
@@ -23,4 +23,6 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
   && timeout -k 10 300 python bench.py --model ViT-B/32 --dtype bf16 --steps 10 --warmup 3 --no-cpu-baseline > $O/configs/c2.json 2> $O/configs/c2.err \
   && timeout -k 10 300 python bench.py --model ViT-L/14@336px --dtype fp16 --steps 5 --warmup 2 --no-cpu-baseline > $O/configs/c4.json 2> $O/configs/c4.err \
   && timeout -k 10 300 python bench.py --model ViT-H-14 --dtype mxfp8 --batch 512 --steps 5 --warmup 2 --no-cpu-baseline > $O/configs/c5.json 2> $O/configs/c5.err \
-  && echo "configs ok"
+  && echo "configs ok" \
+  && timeout -k 10 400 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-profile --ab-splits > $O/configs/c3_ab_splits.json 2>&1 \
+  && echo "ab splits ok"
