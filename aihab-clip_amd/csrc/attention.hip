@@ -1315,10 +1315,6 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, 
   const int nchunks = Npad / 32;
   const size_t lds = (size_t)Npad * 256;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  if (variant == 0) {   // MICLIP_ATTN: falls back where the kernel does not apply
-    variant = 0;
-    if (variant == 9 && (CAUSAL || N < 257 || N > 259)) variant = 0;
-  }
   // two workgroups per CU (default when the queries are 8 full chunks + a small
   // ragged one: K/V (72 KiB) plus the partials of 8 waves x the ragged queries
   // must stay under 80 KiB of LDS, i.e. N - 256 <= 3)

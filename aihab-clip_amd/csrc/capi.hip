@@ -110,8 +110,8 @@ struct miclip_model {
   int dtype = 0;
   // fp16 residual stream (x between blocks), the reference's own fp16 GPU model
   // (clip.load on cuda: convert_weights, clip/model.py:372-393, and the half
-  // activations of VisionTransformer / Transformer). Default with fp16 compute;
-  // MICLIP_RESID_F32=1 keeps an fp32 stream. bf16 compute always streams fp32.
+  // activations of VisionTransformer / Transformer). Default under fp16 and bf16
+  // compute; MICLIP_OPT_RESID_F32 keeps an fp32 stream.
   int resid16 = 0;
   // MICLIP_MXFP8: the vision tower's QKV / c_fc / c_proj run on MX-fp8 operands
   // (gemm_mx.hip); everything else (patch embed, attention, the text tower) as

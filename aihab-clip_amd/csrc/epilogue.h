@@ -134,7 +134,7 @@ struct EpiStore {
   T* C;
   const float* bias;
   int ldc;
-  int nt = 0;   // non-temporal output stores (MICLIP_GEMM_NT, A/B diagnostic)
+  int nt = 0;   // non-temporal output stores (gemm.hip gemm_nt(): off, measured level)
   MICLIP_DEV float4 bias4(int col) const { return ld_bias4(bias, col); }
   MICLIP_DEV float4 bias4nb(int col) const { return ld_bias4_nb(bias, col); }
   MICLIP_DEV float bias1(int col) const { return bias ? bias[col] : 0.f; }

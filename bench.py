@@ -150,6 +150,12 @@ def cpu_baseline(model, cfg, budget_s=12.0, max_images=64):
 
 # ---------------------------------------------------------------- roofline --
 
+def _lib_label():
+    from miclip import _lib
+    here = os.path.relpath(_lib.LIB_PATH, ROOT) if _lib.LIB_PATH.startswith(ROOT) else _lib.LIB_PATH
+    return here if "MICLIP_LIB" in os.environ else f"{here} (in-tree build)"
+
+
 def fc_epilogue(numerics):
     """The c_fc GEMM's epilogue functor as it appears in the kernel symbol."""
     if numerics["mxfp8"]:
@@ -449,7 +455,10 @@ def run(args, backend="nccl", load_model=None):
                        "parallelism": f"dp{world} (image-batch sharding, {args.scaling} scaling)",
                        "splits": model.image_splits(max(hi - lo, 1)),
                        "splits_requested": args.splits, "numerics": model.numerics(),
-                       "weights": "seeded random init, CLIP shapes"},
+                       "weights": "seeded random init, CLIP shapes",
+                       # the library this run loaded (MICLIP_LIB overrides the in-tree
+                       # build for A/B against another revision's binary)
+                       "library": _lib_label()},
             "gflop_per_image": round(gf, 3),
             "path_mfma_frac": round(value * gf * 1e9 / (world * peak * 1e12), 4),
             # FLOPs the kernels execute (the last vision block runs on the CLS rows
