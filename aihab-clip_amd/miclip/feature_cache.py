@@ -385,7 +385,8 @@ def _collective_device(group):
 
 
 @torch.no_grad()
-def gather_shards(local, group=None, width: Optional[int] = None, dtype=torch.float32):
+def gather_shards(local, group=None, width: Optional[int] = None, dtype=torch.float32,
+                  counts: Optional[List[int]] = None):
     """All-gather per-rank row blocks of possibly different lengths, in rank order.
 
     For loaders that hand each rank only its own contiguous slice of a global
@@ -393,7 +394,9 @@ def gather_shards(local, group=None, width: Optional[int] = None, dtype=torch.fl
     all-gather), pad to the longest, all-gather, and drop the padding, so the
     result is the global batch in its original order when rank r holds the r-th
     slice. `local` may be None (an empty shard); then `width` (columns, 0 for a
-    1-D block such as labels) is required. Without a process group: `local`."""
+    1-D block such as labels) is required. `counts` (every rank's row count, when
+    the caller knows them, e.g. shard_range of a known batch) skips the count
+    exchange and the host sync its result needs. Without a process group: `local`."""
     if not (dist.is_available() and dist.is_initialized()):
         return local
     world = dist.get_world_size(group)
@@ -404,10 +407,14 @@ def gather_shards(local, group=None, width: Optional[int] = None, dtype=torch.fl
         dtype = local.dtype
     if width is None:
         raise ValueError("gather_shards needs `width` when a rank has an empty shard")
-    counts = torch.empty(world, dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(counts, torch.tensor([n_local], dtype=torch.int64, device=dev),
-                                group=group)
-    counts = counts.tolist()
+    if counts is None:
+        counts = torch.empty(world, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(counts, torch.tensor([n_local], dtype=torch.int64, device=dev),
+                                    group=group)
+        counts = counts.tolist()
+    elif len(counts) != world or counts[dist.get_rank(group)] != n_local:
+        raise ValueError(f"counts {counts} do not match this rank's {n_local} rows / world {world}")
+    counts = [int(c) for c in counts]
     per = max(counts)
     shape = (per, width) if width else (per,)
     buf = torch.zeros(shape, dtype=dtype, device=dev)

@@ -3,12 +3,13 @@
 
 One step = the hot path of the reference's feature-cache loop
 (aihab_utils/feature_cache.py:114-142 / methods/utils.py:142-173) over one
-device-resident global batch, through the product's sharded driver
-(miclip.feature_cache.sharded_encode):
-    each rank encodes its contiguous slice (encode_image, all HIP kernels,
-    L2-normalise fused into ln_post)
+device-resident global batch, sharded by image as the product's per-rank
+driver does (ShardedBatchLoader + gather_shards):
+    each rank holds and encodes only its contiguous slice (encode_image, all
+    HIP kernels, L2-normalise fused into ln_post)
     -> RCCL all-gather of the normalised embeddings back into the global row
-       order (N > 1; aihab_utils/feature_cache.py:144-162)
+       order (miclip.feature_cache.gather_shards; N > 1;
+       aihab_utils/feature_cache.py:144-162)
     -> zero-shot logits of the gathered rows (x @ visual.proj -> normalise
        -> 100 * f @ text_weights -> top-1; methods/ProLIP.py:288-293).
 --scaling weak (default): 256 images per GPU, global batch 256 N.
@@ -259,7 +260,7 @@ def run(args, backend="nccl", load_model=None):
             torch.cuda.synchronize()
 
     from miclip.configs import MODEL_CONFIGS, algorithmic_gflop_per_image, executed_gflop_per_image
-    from miclip.feature_cache import shard_range, sharded_encode
+    from miclip.feature_cache import gather_shards, shard_range
     from miclip.weights import CLIP_MEAN, CLIP_STD
     cfg = MODEL_CONFIGS[args.model]
     R, W = cfg.image_resolution, cfg.vision_width
@@ -274,16 +275,24 @@ def run(args, backend="nccl", load_model=None):
     log(f"[rank {rank}] model loaded in {time.perf_counter() - t_load:.1f}s; "
         f"{hi - lo} of {n_global} images per step on this rank")
 
-    # the global batch of synthetic CLIP-normalised images, identical on every rank
-    # (a deterministic loader), device-resident before timing
-    g = torch.Generator(device=dev).manual_seed(1234)
+    # synthetic CLIP-normalised images, device-resident before timing. Each rank
+    # makes only its own slice [lo, hi) of the global batch, as a per-rank loader
+    # does (feature_cache.ShardedBatchLoader): image i comes from the generator of
+    # its 256-image chunk, so it is the same image on whichever rank makes it
     mean = torch.tensor(CLIP_MEAN, device=dev).view(1, 3, 1, 1)
     std = torch.tensor(CLIP_STD, device=dev).view(1, 3, 1, 1)
-    imgs = torch.empty(n_global, 3, R, R, device=dev)
-    for i in range(0, n_global, 256):
-        u = torch.rand(min(256, n_global - i), 3, R, R, device=dev, generator=g)
-        imgs[i:i + u.shape[0]] = (u - mean) / std
-    del u
+
+    def make_images(a, b):
+        out = torch.empty(max(b - a, 0), 3, R, R, device=dev)
+        for c in range(a // 256, (b + 255) // 256):
+            g = torch.Generator(device=dev).manual_seed(1234 + c)
+            u = torch.rand(min(256, n_global - 256 * c), 3, R, R, device=dev, generator=g)
+            s0, s1 = max(a, 256 * c), min(b, 256 * c + u.shape[0])
+            out[s0 - a:s1 - a] = (u[s0 - 256 * c:s1 - 256 * c] - mean) / std
+        return out
+
+    imgs = make_images(lo, hi)
+    counts = [b - a for a, b in (shard_range(n_global, r, world) for r in range(world))]
 
     # text head once (clip_classifier flow): synthetic prompt tokens -> encode_text
     gt = torch.Generator().manual_seed(7)
@@ -298,11 +307,11 @@ def run(args, backend="nccl", load_model=None):
     tw = torch.nn.functional.normalize(temb, dim=-1).t().contiguous()      # [E, C]
 
     def make_step(m):
-        def enc(x):
-            return m.encode_image(x, normalize=True)
-
         def step():
-            feats = sharded_encode(enc, imgs, dim=W)        # [n_global, W], global row order
+            # this rank's slice, then the RCCL all-gather of the L2-normalised rows
+            # back into the global order (gather_shards), then the zero-shot head
+            local = m.encode_image(imgs, normalize=True) if hi > lo else None
+            feats = gather_shards(local, width=W, counts=counts)   # [n_global, W]
             return m.zero_shot(feats, tw, 100.0, k=1, apply_proj=True)
         return step
 
@@ -329,11 +338,17 @@ def run(args, backend="nccl", load_model=None):
             dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
         return float(dt_t.item())
 
-    # correctness guard on the timed path: the gathered rows are the single-GPU encode
+    # correctness guard on the timed path: the first 4 rows of every rank's slice,
+    # gathered, are the single-GPU encode of those images in global order
     if world > 1:
-        chk = sharded_encode(lambda x: model.encode_image(x, normalize=True), imgs[:64], dim=W)
-        ref = model.encode_image(imgs[:64], normalize=True)
-        assert torch.equal(chk, ref), "sharded encode differs from the single-GPU encode"
+        k = min(4, hi - lo)
+        firsts = [shard_range(n_global, r, world) for r in range(world)]
+        chk = gather_shards(model.encode_image(imgs[:k], normalize=True) if k else None, width=W,
+                            counts=[min(4, b - a) for a, b in firsts])
+        ref_imgs = torch.cat([make_images(a, min(a + 4, b)) for a, b in firsts])
+        ref = model.encode_image(ref_imgs, normalize=True)
+        assert torch.equal(chk.to(ref.device), ref), "gathered rows differ from the single-GPU encode"
+        del ref_imgs
 
     for _ in range(args.warmup):
         step()
@@ -448,7 +463,7 @@ def run(args, backend="nccl", load_model=None):
             "scaling": args.scaling, "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (224px CLIP-normalised uniform noise; seeded random-init weights)",
             "config": {"workload": f"{args.model} feature-cache encode: encode_image bs={per_gpu} "
-                                   f"@{R}px + L2-normalise + RCCL all-gather (sharded_encode) + "
+                                   f"@{R}px + L2-normalise + RCCL all-gather (gather_shards) + "
                                    f"zero-shot logits ({args.classes} classes)",
                        "global_batch": n_global, "images_per_gpu": hi - lo,
                        "tokens_per_image": cfg.n_tokens,

@@ -156,3 +156,46 @@ def test_per_rank_loader_matches_single_process(n, bs):
             want += list(range(b + lo, b + hi))
         assert read == want, "a rank read images outside its own slice"
         assert (feats == ref_f.numpy()).all() and (labels == ref_l.numpy()).all()
+
+
+def _worker_counts(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from miclip.feature_cache import gather_shards, shard_range
+    n = 7
+    counts = [b - a for a, b in (shard_range(n, r, world) for r in range(world))]
+    lo, hi = shard_range(n, rank, world)
+    local = torch.arange(lo * 3, hi * 3, dtype=torch.float32).view(-1, 3)
+    got = gather_shards(local, counts=counts)            # known counts: no count exchange
+    got2 = gather_shards(local)                          # exchanged counts
+    err = None
+    try:
+        gather_shards(local, counts=[counts[0] + 1] + counts[1:] if rank == 0 else counts[::-1])
+    except ValueError as e:
+        err = str(e)
+    q.put((rank, got.numpy(), got2.numpy(), err))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_shards_known_counts():
+    """gather_shards(counts=...) (bench.py's step: the slices of a known batch) gives
+    the exchanged-count result without its host sync; wrong counts are refused."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world, port = 2, _free_port()
+    procs = [ctx.Process(target=_worker_counts, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, a, b, err = q.get(timeout=120)
+        res[r] = (a, b, err)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = torch.arange(21, dtype=torch.float32).view(7, 3).numpy()
+    for r in range(world):
+        a, b, err = res[r]
+        assert (a == want).all() and (b == want).all()
+        assert err is not None and "counts" in err
