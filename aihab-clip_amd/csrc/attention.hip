@@ -545,6 +545,73 @@ __global__ __launch_bounds__(576) void attention80s_kernel(const T* __restrict__
   }
 }
 
+#ifdef MICLIP_EXPERIMENTS
+// Experimental (measured level with attention_kernel<64> at N = 577: 0.321-0.349 vs
+// 0.315-0.371 ms per B = 128 launch), diagnostic library only.
+// Head dim 64, N > 320 (ViT-L/14@336: N = 577, C4): attention_kernel<64>'s
+// one head per workgroup (K/V 152 KiB: one workgroup per CU) with the head's fetch in
+// two phases, as attention80s_kernel does. Each wave first loads the Q fragments of
+// its first chunk and retires them (so hipcc's own count for those loads never covers
+// a DMA), then the K/V pieces of key tiles [0, TA) and the rest; it waits for its own
+// phase-A pieces, the workgroup syncs, and the first chunk runs over tiles [0, TA)
+// while phase B lands; a full wait + barrier, the rest of the first chunk, then the
+// wave's further chunks as in attention_kernel. Same tiles in the same order per
+// chunk: bit-identical to attention_kernel<64> (non-causal).
+template <typename T>
+__global__ __launch_bounds__(640) void attention_2p_kernel(const T* __restrict__ qkv,
+                                                           T* __restrict__ out, int N, int H,
+                                                           int Npad, int nchunks, float qk_scale,
+                                                           int prio) {
+  using G = HeadGeom<64>;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  char* kimg = smem;
+  char* vimg = smem + Npad * G::ROWB;
+  const int bh = blockIdx.x;
+  const int b = bh / H, h = bh - b * H;
+  const int D = H * 64, ld = 3 * D;
+  const T* base = qkv + (size_t)b * N * ld + h * 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int nkt = Npad >> 5, TA = nkt / 2;
+  const float c2 = qk_scale * kLog2e;
+  const int c0 = wave;
+  i16x8 qf[G::NKS];
+  load_q<T, 64>(qf, base, ld, c0 < nchunks ? c0 : 0, N, lane);
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
+  const int prow = lane >> 3, pch = lane & 7, pieces = Npad / 8, pa = TA * 4;
+  auto kv_piece = [&](bool isv, int piece) {
+    const int row = piece * 8 + prow;
+    const int r = row < N ? row : N - 1;
+    const int lch = isv ? (pch ^ ((row & 3) << 1)) : (pch ^ ((row >> 1) & 7));
+    glds16_hidden(base + (size_t)r * ld + (isv ? 2 * D : D) + lch * 8,
+                  (isv ? vimg : kimg) + piece * 1024);
+  };
+  const int nA = 2 * pa, nB = 2 * (pieces - pa), half = pieces - pa;
+  for (int pc = wave; pc < nA; pc += nw) kv_piece(pc >= pa, pc >= pa ? pc - pa : pc);
+  for (int pc = wave; pc < nB; pc += nw) kv_piece(pc >= half, pa + (pc >= half ? pc - half : pc));
+  wait_vm_upto(wave < nB ? (nB - wave + nw - 1) / nw : 0);   // this wave's phase A landed
+  __syncthreads();
+  f32x16 o[G::NDT];
+  float lsum = 0.f, m = 0.f;
+  if (c0 < nchunks)
+    attend_chunk<T, false, 64>(kimg, vimg, qf, c0, N, Npad, c2, lane, o, lsum, m, 0, TA, prio,
+                               true, false);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  T* obase = out + (size_t)b * N * D + h * 64;
+  if (c0 < nchunks) {
+    attend_chunk<T, false, 64>(kimg, vimg, qf, c0, N, Npad, c2, lane, o, lsum, m, TA, -1, prio,
+                               false, true);
+    attend_store<T, 64>(o, lsum, c0, N, obase, D, lane);
+  }
+  for (int chunk = c0 + nw; chunk < nchunks; chunk += nw) {
+    load_q<T, 64>(qf, base, ld, chunk, N, lane);
+    attend_chunk<T, false, 64>(kimg, vimg, qf, chunk, N, Npad, c2, lane, o, lsum, m, 0, -1,
+                               prio);
+    attend_store<T, 64>(o, lsum, chunk, N, obase, D, lane);
+  }
+}
+#endif  // MICLIP_EXPERIMENTS
+
 // ---------------------------------------------------------------------------
 // Pipelined form: one workgroup walks hpw consecutive (image, head) pairs.
 // While head j is computed, head j+1's K and V are LDS-DMA'd
@@ -1393,7 +1460,7 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, 
   }
   // pipelined kernel (default; variant 2): two K/V buffers must fit in LDS
   // (N <= 320). ViT-L/14 layer: 0.19-0.21 ms vs 0.21-0.24 ms one head per WG.
-  if (variant != 1 && 2 * lds + 2 * 10 * 2 * 66 * 4 <= 160 * 1024) {
+  if (variant != 1 && variant != 3 && 2 * lds + 2 * 10 * 2 * 66 * 4 <= 160 * 1024) {
     static bool attr_set = false;
     if (!attr_set) {
       for (const void* k : {(const void*)attention_pipe_kernel<T, CAUSAL, false>,
@@ -1432,6 +1499,24 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, 
                          attn_prio());
     return hipGetLastError();
   }
+#ifdef MICLIP_EXPERIMENTS
+  // variant 3: the two-phase one-head-per-workgroup kernel (experiments library)
+  if (!CAUSAL && variant == 3 && nchunks >= 4 && lds <= 160 * 1024) {
+    static bool a2p = false;
+    if (!a2p) {
+      const hipError_t e = hipFuncSetAttribute((const void*)attention_2p_kernel<T>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               160 * 1024);
+      if (e != hipSuccess) return e;
+      a2p = true;
+    }
+    const int per = (nchunks + 9) / 10, nw = (nchunks + per - 1) / per;
+    hipLaunchKernelGGL((attention_2p_kernel<T>), dim3(B * H), dim3(nw * 64), lds, s,
+                       (const T*)qkv, (T*)out, N, H, Npad, nchunks, 0.125f, attn_prio());
+    return hipGetLastError();
+  }
+#endif  // MICLIP_EXPERIMENTS
+  if (variant == 3) return hipErrorInvalidValue;
   return attn_launch_plain<T, CAUSAL, 64>(qkv, out, B, N, H, s);
 }
 

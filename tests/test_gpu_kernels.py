@@ -366,6 +366,41 @@ def test_attention_dh80(lib, dt, B, N, H, causal):
 
 
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
+@pytest.mark.parametrize("B,N,H", [(2, 577, 16), (3, 400, 4), (1, 608, 2), (2, 330, 3), (5, 257, 2),
+                                   (1, 128, 1)])
+def test_attention_two_phase_dh64_bitexact(lib, exp_lib, dt, B, N, H):
+    """The two-phase one-head-per-workgroup kernel (variant 3, experiments library:
+    measured level with attention_kernel<64>; first chunk's Q retired before the K/V
+    DMAs, key tiles [0, TA) computed while the rest lands) equals attention_kernel<64>
+    (variant 1) bit for bit, and fp32 SDPA within the kernel tolerance; the product
+    library refuses variant 3."""
+    code, tdt = DT[dt]
+    z = torch.zeros(N * 3 * 64, device="cuda", dtype=tdt)
+    assert lib.miclip_op_attention(code, z.data_ptr(), z.data_ptr(), 1, N, 1, 64, 0, 3,
+                                   _stream()) != 0
+    lib = exp_lib
+    g = torch.Generator(device="cuda").manual_seed(B * 1000 + N + H + 641)
+    qkv = (torch.randn(B * N, 3 * H * 64, device="cuda", generator=g) * 1.5).to(tdt)
+    outs = []
+    for v in (1, 3):
+        out = torch.full((B * N + 1, H * 64), 7.0, device="cuda", dtype=tdt)
+        _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), out.data_ptr(), B, N, H, 64, 0,
+                                            v, _stream()))
+        outs.append(out)
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)
+    assert bool((outs[1][B * N] == 7.0).all())
+    ref = _attn_ref(qkv, B, N, H, False)
+    err = (outs[1][:B * N].float() - ref).abs().max().item()
+    assert err < (4e-2 if dt == "bf16" else 6e-3), err
+    x = torch.zeros(77, 3 * 64, device="cuda", dtype=tdt)   # causal: refused
+    y = torch.zeros(77, 64, device="cuda", dtype=tdt)
+    assert lib.miclip_op_attention(code, x.data_ptr(), y.data_ptr(), 1, 77, 1, 64, 1, 3,
+                                   _stream()) != 0
+
+
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
 @pytest.mark.parametrize("B,N,H", [(2, 257, 16), (3, 160, 4), (1, 288, 2), (4, 200, 3), (64, 257, 16)])
 def test_attention_dh80_two_phase_bitexact(lib, dt, B, N, H):
     """The two-phase head-dim-80 kernel (default, variant 2: Q by LDS-DMA, key tiles 0-3
