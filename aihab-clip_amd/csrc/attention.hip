@@ -367,12 +367,13 @@ MICLIP_DEV void load_q(i16x8 (&qf)[HeadGeom<DH>::NKS], const T* base, int ld, in
   for (int s = 0; s < HeadGeom<DH>::NKS; ++s) qf[s] = *(const i16x8*)(qp + 16 * s);
 }
 
-// One workgroup per (image, head). Launch bounds: 10 waves for DH = 64 (3
-// per SIMD, ~165 VGPRs); DH = 80 carries a third O^T tile and a fifth Q
+// One workgroup per (image, head). Launch bounds: NWMAX waves -- DH = 64: 12
+// (3 per SIMD, 132 VGPRs) or 16 (4 per SIMD, 128 VGPRs, one spill outside the key
+// loop), see attn_launch_plain; DH = 80 carries a third O^T tile and a fifth Q
 // fragment and just fits the 168 VGPRs of 9 waves (3 on one SIMD): one wave
 // per 32-query chunk at N = 257 (8 waves left one wave two chunks).
-template <typename T, bool CAUSAL, int DH>
-__global__ __launch_bounds__(DH == 64 ? 640 : 576) void attention_kernel(
+template <typename T, bool CAUSAL, int DH, int NWMAX = (DH == 64 ? 12 : 9)>
+__global__ __launch_bounds__(NWMAX * 64) void attention_kernel(
     const T* __restrict__ qkv, T* __restrict__ out, int N, int H, int Npad, int nchunks,
     float qk_scale, int prio) {
   using G = HeadGeom<DH>;
@@ -1329,23 +1330,44 @@ constexpr int attn_prio() { return 1; }
 
 // one workgroup per (image, head)
 template <typename T, bool CAUSAL, int DH>
-hipError_t attn_launch_plain(const void* qkv, void* out, int B, int N, int H, hipStream_t s) {
+hipError_t attn_launch_plain(const void* qkv, void* out, int B, int N, int H, hipStream_t s,
+                             int waves = 0) {
   using G = HeadGeom<DH>;
   const int Npad = (N + 31) & ~31;
   const int nchunks = Npad / 32;
   const size_t lds = (size_t)Npad * G::ROWB * 2;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  // at most 10 (DH 64) / 9 (DH 80) waves, see attention_kernel's launch bounds
-  constexpr int maxw = DH == 64 ? 10 : 9;
-  const int per = (nchunks + maxw - 1) / maxw;
-  const int nw = (nchunks + per - 1) / per;
-  auto kern = attention_kernel<T, CAUSAL, DH>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute(
-        (const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  // Waves: DH 80 at most 9 (the fewest that keep the chunks per wave). DH 64: one
+  // per chunk up to 16 (4 per SIMD, attention_kernel<.., 16>). A wave's chunks run
+  // serially and a SIMD's waves share its issue, so the count sets both the longest
+  // chain and the per-SIMD load: at N = 577 (18 full chunks + one 1-query chunk)
+  // 10 waves put 6 chunks on one SIMD (waves 0, 4, 8), 12 or 16 waves at most 5 --
+  // 0.312-0.322 (10) -> 0.287-0.303 (12) / 0.284-0.296 ms (16) per B = 128 launch,
+  // bit-identical (scripts/probe/attn_waves.py, profiles/r04/configs/attn577_waves.jsonl).
+  // `waves` (variants 10-16) forces a count for that probe.
+  int nw;
+  if constexpr (DH == 64) {
+    nw = nchunks < 16 ? nchunks : 16;
+    if (waves > 0) {
+      if (waves > 16) return hipErrorInvalidValue;
+      nw = waves < nchunks ? waves : nchunks;
+    }
+  } else {
+    if (waves > 0) return hipErrorInvalidValue;
+    const int per = (nchunks + 8) / 9;
+    nw = (nchunks + per - 1) / per;
+  }
+  void (*kern)(const T*, T*, int, int, int, int, float, int);
+  if constexpr (DH == 64)
+    kern = nw > 12 ? attention_kernel<T, CAUSAL, DH, 16> : attention_kernel<T, CAUSAL, DH, 12>;
+  else
+    kern = attention_kernel<T, CAUSAL, DH>;
+  static bool attr_set[2] = {false, false};
+  if (!attr_set[nw > 12]) {
+    const hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
-    attr_set = true;
+    attr_set[nw > 12] = true;
   }
   hipLaunchKernelGGL(kern, dim3(B * H), dim3(nw * 64), lds, s, (const T*)qkv, (T*)out, N, H,
                      Npad, nchunks, 1.0f / sqrtf((float)DH), attn_prio());
@@ -1460,7 +1482,7 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, 
   }
   // pipelined kernel (default; variant 2): two K/V buffers must fit in LDS
   // (N <= 320). ViT-L/14 layer: 0.19-0.21 ms vs 0.21-0.24 ms one head per WG.
-  if (variant != 1 && variant != 3 && 2 * lds + 2 * 10 * 2 * 66 * 4 <= 160 * 1024) {
+  if (variant != 1 && variant != 3 && variant < 10 && 2 * lds + 2 * 10 * 2 * 66 * 4 <= 160 * 1024) {
     static bool attr_set = false;
     if (!attr_set) {
       for (const void* k : {(const void*)attention_pipe_kernel<T, CAUSAL, false>,
@@ -1517,7 +1539,7 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, 
   }
 #endif  // MICLIP_EXPERIMENTS
   if (variant == 3) return hipErrorInvalidValue;
-  return attn_launch_plain<T, CAUSAL, 64>(qkv, out, B, N, H, s);
+  return attn_launch_plain<T, CAUSAL, 64>(qkv, out, B, N, H, s, variant >= 10 ? variant : 0);
 }
 
 }  // namespace

@@ -95,8 +95,9 @@ hipError_t ln_fold(int dtype, const void* W, const float* gamma, const float* be
 // (clip/model.py:323-329). variant (dh 64): 0 = default (the two-workgroup x8
 // kernel for N in 256..259, else the pipelined multi-head kernel when N <= 320,
 // one head per workgroup above), 1 = one head per workgroup, 2 = pipelined,
-// 4 = pipelined + last-chunk split, 8 = x8. variant (dh 80): 0 = default (the
-// two-phase kernel where it applies), 1 = attention_kernel<80>, 2 = two-phase.
+// 4 = pipelined + last-chunk split, 8 = x8, 10-16 = one head per workgroup on
+// that many waves (probe). variant (dh 80): 0 = default (the two-phase kernel where
+// it applies), 1 = attention_kernel<80>, 2 = two-phase.
 hipError_t attention(int dtype, const void* qkv, void* out, int B, int N, int H, int causal,
                      hipStream_t s, int variant = 0, int head_dim = 64);
 

@@ -426,6 +426,31 @@ def test_attention_dh80_two_phase_bitexact(lib, dt, B, N, H):
 
 
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
+@pytest.mark.parametrize("B,N,H", [(2, 577, 16), (1, 640, 2), (3, 352, 3)])
+def test_attention_one_head_wave_counts(lib, dt, B, N, H):
+    """attention_kernel<64> (one head per workgroup, N > 320) on a forced number of waves
+    (variants 10-16) equals the default (variant 1: one wave per chunk up to 16) bit
+    for bit: a chunk's arithmetic does not depend on which wave runs it. 17 is refused."""
+    code, tdt = DT[dt]
+    g = torch.Generator(device="cuda").manual_seed(B * 1000 + N + H + 1616)
+    qkv = (torch.randn(B * N, 3 * H * 64, device="cuda", generator=g) * 1.5).to(tdt)
+    outs = []
+    for v in (1, 10, 12, 13, 16):
+        out = torch.full((B * N + 1, H * 64), 7.0, device="cuda", dtype=tdt)
+        _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), out.data_ptr(), B, N, H, 64, 0,
+                                            v, _stream()))
+        outs.append(out)
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    assert bool((outs[0][B * N] == 7.0).all())
+    ref = _attn_ref(qkv, B, N, H, 0)
+    assert (outs[0][:B * N].float() - ref).abs().max().item() < (4e-2 if dt == "bf16" else 6e-3)
+    assert lib.miclip_op_attention(code, qkv.data_ptr(), outs[0].data_ptr(), B, N, H, 64, 0, 17,
+                                   _stream()) != 0
+
+
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
 @pytest.mark.parametrize("B,N,H,dh", [(3, 257, 16, 64), (2, 577, 16, 64), (5, 50, 12, 64),
                                       (2, 257, 16, 80), (1, 1, 1, 64), (2, 640, 2, 64), (1, 768, 2, 80),
                                       (7, 197, 3, 64), (1, 65, 5, 80)])
