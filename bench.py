@@ -429,7 +429,9 @@ def run(args, backend="nccl", load_model=None):
             M = (hi - lo) * cfg.n_tokens
             epi = fc_epilogue(model.numerics())
             traffic, tsrc = attach_traffic(args.model, args.dtype, epi, M)
-            act_name = "exact-GELU" if cfg.act == "erf" else "QuickGELU"
+            nm = model.numerics()
+            act_name = ("QuickGELU" if cfg.act != "erf" else
+                        "GELU, tanh form" if nm.get("mxfp8") and nm.get("mx_gelu_tanh") else "exact GELU")
             roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": round(peak, 1),
                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
                         "kernel": f"gemm_fc: MLP c_fc GEMM, {epi} epilogue + {act_name}"
