@@ -179,6 +179,53 @@ def test_layernorm(lib, dt, R, D):
     assert (outt.float() - ref).abs().max().item() < (3e-2 if dt == "bf16" else 4e-3)
 
 
+@pytest.mark.parametrize("D", [1024, 1280])
+def test_layernorm_row_paths_bitexact(lib, D):
+    """fp16-stream LayerNorm launches of >= 1024 x 32 rows take 32-row workgroups (each wave
+    4 row pairs), smaller ones 8-row workgroups: the same per-row arithmetic, so a row's
+    output is identical whichever path ran it -- fp16 out, fp16 in place, and (D = 1280)
+    MX-fp8 rows and scales. R odd: the last pair's second row is past the end."""
+    R = 33001
+    g = torch.Generator(device="cuda").manual_seed(D)
+    x = ((torch.randn(R, D, device="cuda", generator=g) * 3 + 0.5)).half()
+    gam = 1 + 0.1 * torch.randn(D, device="cuda", generator=g)
+    bet = 0.05 * torch.randn(D, device="cuda", generator=g)
+    full = torch.empty(R, D, device="cuda", dtype=torch.float16)
+    _check(lib, lib.miclip_op_layernorm(0, x.data_ptr(), gam.data_ptr(), bet.data_ptr(),
+                                        full.data_ptr(), 2, R, D, _stream()))
+    xin = x.clone()
+    _check(lib, lib.miclip_op_layernorm(0, xin.data_ptr(), gam.data_ptr(), bet.data_ptr(),
+                                        xin.data_ptr(), 2, R, D, _stream()))
+    lo, hi = (0, 1024), (R - 233, R)
+    parts = []
+    for a, b in (lo, hi):
+        o = torch.empty(b - a, D, device="cuda", dtype=torch.float16)
+        _check(lib, lib.miclip_op_layernorm(0, x[a:b].data_ptr(), gam.data_ptr(), bet.data_ptr(),
+                                            o.data_ptr(), 2, b - a, D, _stream()))
+        parts.append(o)
+    torch.cuda.synchronize()
+    assert torch.equal(xin, full)
+    assert torch.equal(parts[0], full[:1024]) and torch.equal(parts[1], full[R - 233:])
+    ref = torch.nn.functional.layer_norm(x.float(), (D,), gam, bet, 1e-5)
+    assert (full.float() - ref).abs().max().item() < 4e-3
+    if D % 128 == 0 and D == 1280:
+        sb = int(lib.miclip_mx_scale_bytes(R, D))
+        q = torch.empty(R, D, dtype=torch.uint8, device="cuda")
+        sc = torch.zeros(sb, dtype=torch.uint8, device="cuda")
+        _check(lib, lib.miclip_op_layernorm_mx(x.data_ptr(), 1, gam.data_ptr(), bet.data_ptr(),
+                                               q.data_ptr(), sc.data_ptr(), R, D, _stream()))
+        blk = (D // 128) * 1024            # scale bytes per 256-row block
+        for a, b in ((0, 1024), (32768, R)):   # slices start on a 256-row block
+            qa = torch.empty(b - a, D, dtype=torch.uint8, device="cuda")
+            sa = torch.zeros(int(lib.miclip_mx_scale_bytes(b - a, D)), dtype=torch.uint8, device="cuda")
+            _check(lib, lib.miclip_op_layernorm_mx(x[a:b].data_ptr(), 1, gam.data_ptr(), bet.data_ptr(),
+                                                   qa.data_ptr(), sa.data_ptr(), b - a, D, _stream()))
+            torch.cuda.synchronize()
+            assert torch.equal(qa, q[a:b])
+            nb = (b - a + 255) // 256
+            assert torch.equal(sa[:nb * blk], sc[a // 256 * blk:(a // 256 + nb) * blk])
+
+
 @pytest.mark.parametrize("R,D", [(7, 768), (513, 1024), (3, 1280), (300, 1536)])
 def test_layernorm_fp16_stream(lib, R, D):
     """fp16 input (the fp16 residual stream): fp32 out, fp16 out, and fp16 in place (ln_pre)."""
