@@ -37,7 +37,8 @@ if [ "${1:-}" = attn ]; then
 fi
 if [ "${1:-}" = bench ]; then
   # every kernel of the benched step (one unsplit step: --splits 1)
-  CMD=(python3 bench.py --steps 1 --warmup 0 --splits 1 --no-cpu-baseline --no-profile)
+  # PMC_BENCH_ARGS: extra bench.py arguments (e.g. "--model ViT-L/14@336px" for C4)
+  CMD=(python3 bench.py --steps 1 --warmup 0 --splits 1 --no-cpu-baseline --no-profile ${PMC_BENCH_ARGS:-})
   i=0
   for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE" \
              "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_SALU" \
