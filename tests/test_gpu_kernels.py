@@ -473,28 +473,30 @@ def test_attention_dh80_two_phase_bitexact(lib, dt, B, N, H):
 
 
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
-@pytest.mark.parametrize("B,N,H", [(2, 577, 16), (1, 640, 2), (3, 352, 3)])
-def test_attention_one_head_wave_counts(lib, dt, B, N, H):
+@pytest.mark.parametrize("B,N,H,causal", [(2, 577, 16, 0), (1, 640, 2, 0), (3, 352, 3, 0),
+                                          (2, 400, 2, 1), (1, 577, 3, 1)])
+def test_attention_one_head_wave_counts(lib, dt, B, N, H, causal):
     """attention_kernel<64> (one head per workgroup, N > 320) on a forced number of waves
     (variants 10-16) equals the default (variant 1: one wave per chunk up to 16) bit
-    for bit: a chunk's arithmetic does not depend on which wave runs it. 17 is refused."""
+    for bit: a chunk's arithmetic does not depend on which wave runs it (causal too,
+    where chunks carry unequal work). 17 is refused."""
     code, tdt = DT[dt]
-    g = torch.Generator(device="cuda").manual_seed(B * 1000 + N + H + 1616)
+    g = torch.Generator(device="cuda").manual_seed(B * 1000 + N + H + 1616 + causal)
     qkv = (torch.randn(B * N, 3 * H * 64, device="cuda", generator=g) * 1.5).to(tdt)
     outs = []
     for v in (1, 10, 12, 13, 16):
         out = torch.full((B * N + 1, H * 64), 7.0, device="cuda", dtype=tdt)
-        _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), out.data_ptr(), B, N, H, 64, 0,
-                                            v, _stream()))
+        _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), out.data_ptr(), B, N, H, 64,
+                                            causal, v, _stream()))
         outs.append(out)
     torch.cuda.synchronize()
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
     assert bool((outs[0][B * N] == 7.0).all())
-    ref = _attn_ref(qkv, B, N, H, 0)
+    ref = _attn_ref(qkv, B, N, H, causal)
     assert (outs[0][:B * N].float() - ref).abs().max().item() < (4e-2 if dt == "bf16" else 6e-3)
-    assert lib.miclip_op_attention(code, qkv.data_ptr(), outs[0].data_ptr(), B, N, H, 64, 0, 17,
-                                   _stream()) != 0
+    assert lib.miclip_op_attention(code, qkv.data_ptr(), outs[0].data_ptr(), B, N, H, 64, causal,
+                                   17, _stream()) != 0
 
 
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
