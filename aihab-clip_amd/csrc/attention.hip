@@ -22,9 +22,10 @@
 //   * K image XOR-swizzled by (row>>1)&7 (conflict-free ds_read_b128 for the
 //     32x32x16 A fragment), V image by (row&3)<<1 (conflict-free tr reads);
 //     both layouts were checked with an LDS bank model of gfx950's lane groups.
-//   * head dim 80 (HeadGeom<80>): K/V rows padded to 96 dims (192 B); S^T takes
-//     5 k-steps, O^T three 32-dim tiles of which the last is half padding
-//     (zero V columns, never stored).
+//   * head dim 80 (HeadGeom<80>): K/V rows padded to 96 dims (192 B; K chunks
+//     rotated by (row >> 3) & 3, V unswizzled -- conflict-free at that pitch, see
+//     HeadGeom); S^T takes 5 k-steps, O^T three 32-dim tiles of which the last is
+//     half padding (zero V columns, never stored).
 #include "common.h"
 #include "kernels.h"
 
@@ -61,11 +62,18 @@ MICLIP_DEV float xor32_sum(float x) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// LDS geometry of one (image, head)'s K or V image for head dim DH.
-// DH = 64: 128-B rows of 8 16-B chunks, the swizzles XOR over all 8.
-// DH = 80: rows padded to 96 dims (192 B, 12 chunks); chunks 0-7 swizzle as
-// for 64, chunks 8-11 among themselves (x & 3), so the map stays a bijection
-// per row and the lane-invariant offsets of attend_chunk still hold.
+// LDS geometry of one (image, head)'s K or V image for head dim DH: where logical
+// 16-B chunk c of key row `row` sits (kswz / vswz) and which logical chunk a
+// physical one holds (kinv / vinv, for the source-side swizzle of the LDS-DMA).
+// DH = 64: 128-B rows of 8 chunks; K XOR (row >> 1) & 7, V XOR (row & 3) << 1.
+// DH = 80: rows padded to 96 dims (192 B, 12 chunks, a 48-dword pitch): K rotated
+// by (row >> 3) & 3 chunks, V unswizzled. Bank model (MI355X_MICROARCH.md LDS
+// table): attend_chunk's K ds_read_b128 (rows l32, chunk 2s + hh) and V
+// ds_read_b64_tr_b16 (rows 4 (g >> 1) + tq, +8, +16) are then conflict-free --
+// 20 / 24 LDS cycles per tile instead of the 40 / 40 of the XOR swizzle the 128-B
+// rows use, which is 2-way at this pitch (PMC: SQ_LDS_BANK_CONFLICT 45 % of the
+// LDS-active cycles of the head-dim-80 kernel before). V's swizzle must not move
+// with row bits 3-4: attend_chunk reads rows +8 / +16 at fixed offsets.
 template <int DH>
 struct HeadGeom {
   static_assert(DH == 64 || DH == 80, "head dim 64 or 80");
@@ -74,10 +82,21 @@ struct HeadGeom {
   static constexpr int ROWB = NDT * 64;       // LDS bytes per key row
   static constexpr int CH = ROWB / 16;        // 16-B chunks per row
   static constexpr int TILEB = 32 * ROWB;     // one 32-key tile
-  // physical chunk of logical chunk c under the row's swizzle key x (0..7)
-  static MICLIP_DEV int swz(int c, int x) {
-    return (ROWB == 128 || c < 8) ? (c ^ x) : 8 + ((c - 8) ^ (x & 3));
+  static MICLIP_DEV int kswz(int c, int row) {
+    if constexpr (DH == 64) return c ^ ((row >> 1) & 7);
+    const int p = c + ((row >> 3) & 3);
+    return p < 12 ? p : p - 12;
   }
+  static MICLIP_DEV int kinv(int p, int row) {
+    if constexpr (DH == 64) return p ^ ((row >> 1) & 7);
+    const int c = p - ((row >> 3) & 3);
+    return c >= 0 ? c : c + 12;
+  }
+  static MICLIP_DEV int vswz(int c, int row) {
+    if constexpr (DH == 64) return c ^ ((row & 3) << 1);
+    return c;
+  }
+  static MICLIP_DEV int vinv(int p, int row) { return vswz(p, row); }   // involutions
 };
 
 // One wave: 32 queries [32*chunk, +32) of one (image, head) against all keys
@@ -117,12 +136,12 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
   int koff[G::NKS];
 #pragma unroll
   for (int s = 0; s < G::NKS; ++s)
-    koff[s] = l32 * G::ROWB + (G::swz(2 * s + hh, (l32 >> 1) & 7) << 4);
+    koff[s] = l32 * G::ROWB + (G::kswz(2 * s + hh, l32) << 4);
   int voff[G::NDT];
 #pragma unroll
   for (int dt = 0; dt < G::NDT; ++dt) {
     const int ch = 4 * dt + 2 * (g & 1) + (tp >> 1);
-    voff[dt] = (4 * (g >> 1) + tq) * G::ROWB + (G::swz(ch, tq << 1) << 4) + 8 * (tp & 1);
+    voff[dt] = (4 * (g >> 1) + tq) * G::ROWB + (G::vswz(ch, 4 * (g >> 1) + tq) << 4) + 8 * (tp & 1);
   }
   // Two-stage tile pipeline (cdna_hip_programming.md T15): the S^T MFMAs of
   // tile kt+1 are issued before tile kt's softmax, so the matrix pipe works
@@ -407,8 +426,8 @@ __global__ __launch_bounds__(NWMAX * 64) void attention_kernel(
   } else {
     // head dim 80: the same all-DMAs-then-one-wait staging over 192-B rows. A
     // 1-KiB piece covers 5 1/3 rows, so each lane finds the (row, physical chunk)
-    // its 16 bytes land on and fetches the logical chunk there (the swizzle is an
-    // involution: swz(swz(c, x), x) == c). Padding chunks (dims 80-95) take dims
+    // its 16 bytes land on and fetches the logical chunk there (HeadGeom::kinv /
+    // vinv, the inverse swizzles). Padding chunks (dims 80-95) take dims
     // 16-31 of the same row -- finite; K's are never read (5 k-steps cover dims
     // 0-79), V's only feed O^T rows 80-95, which are never stored. Pad rows repeat
     // row N - 1. (The register path this replaces loaded 2 x 16 B per thread and
@@ -420,7 +439,7 @@ __global__ __launch_bounds__(NWMAX * 64) void attention_kernel(
       const int piece = isv ? pc - pieces : pc;
       const int off = piece * 1024 + lane * 16;
       const int row = off / G::ROWB, pch = (off - row * G::ROWB) >> 4;
-      int c = G::swz(pch, isv ? ((row & 3) << 1) : ((row >> 1) & 7));
+      int c = isv ? G::vinv(pch, row) : G::kinv(pch, row);
       const T* src;
       if (isv && c == DH / 8) {   // V dims 80-87: ones (the row sum, see kOnesF16)
         src = (const T*)(std::is_same_v<T, _Float16> ? kOnesF16 : kOnesBF16);
@@ -494,7 +513,7 @@ __global__ __launch_bounds__(576) void attention80s_kernel(const T* __restrict__
   auto kv_piece = [&](bool isv, int piece) {
     const int off = piece * 1024 + lane * 16;
     const int row = off / G::ROWB, pch = (off - row * G::ROWB) >> 4;
-    int c = G::swz(pch, isv ? ((row & 3) << 1) : ((row >> 1) & 7));
+    int c = isv ? G::vinv(pch, row) : G::kinv(pch, row);
     const T* src;
     if (isv && c == 80 / 8) {
       src = (const T*)(std::is_same_v<T, _Float16> ? kOnesF16 : kOnesBF16);
