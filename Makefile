@@ -38,22 +38,7 @@ stamps: $(OBJS)
 	$(HIPCC) $(HIPFLAGS) -c scripts/stamps/stamp_gemm_kloop.hip -o build/stamps/stamp_gemm_kloop.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) build/stamps/stamp_gemm_kloop.o $(filter-out $(OBJ_DIR)/gemm.o,$(OBJS)) -o build/stamps/libstamp_gemm_kloop.so
 
-# diagnostic library with the measured-slower experimental kernels (gemm.hip /
-# attention.hip MICLIP_EXPERIMENTS: ping-pong, 256x128, 4-wave GEMMs, streamed
-# attention); tests and A/B scripts load it explicitly (MICLIP_LIB or
-# _lib.load_library(path)), the product libmiclip.so never contains them
-EXP_DIR  := build/exp
-EXP_OBJS := $(patsubst $(SRC_DIR)/%.hip,$(EXP_DIR)/obj/%.o,$(SRCS))
-EXP_LIB  := $(EXP_DIR)/libmiclip_exp.so
-$(EXP_DIR)/obj/attention.o: HIPFLAGS += -fno-honor-nans -fno-slp-vectorize
-$(EXP_DIR)/obj/%.o: $(SRC_DIR)/%.hip $(HDRS)
-	@mkdir -p $(EXP_DIR)/obj
-	$(HIPCC) $(HIPFLAGS) -DMICLIP_EXPERIMENTS -c $< -o $@
-$(EXP_LIB): $(EXP_OBJS)
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(EXP_OBJS) -o $@
-exp: $(EXP_LIB)
-
 clean:
 	rm -rf build $(LIB)
 
-.PHONY: all clean asm stamps exp
+.PHONY: all clean asm stamps

@@ -565,72 +565,6 @@ __global__ __launch_bounds__(576) void attention80s_kernel(const T* __restrict__
   }
 }
 
-#ifdef MICLIP_EXPERIMENTS
-// Experimental (measured level with attention_kernel<64> at N = 577: 0.321-0.349 vs
-// 0.315-0.371 ms per B = 128 launch), diagnostic library only.
-// Head dim 64, N > 320 (ViT-L/14@336: N = 577, C4): attention_kernel<64>'s
-// one head per workgroup (K/V 152 KiB: one workgroup per CU) with the head's fetch in
-// two phases, as attention80s_kernel does. Each wave first loads the Q fragments of
-// its first chunk and retires them (so hipcc's own count for those loads never covers
-// a DMA), then the K/V pieces of key tiles [0, TA) and the rest; it waits for its own
-// phase-A pieces, the workgroup syncs, and the first chunk runs over tiles [0, TA)
-// while phase B lands; a full wait + barrier, the rest of the first chunk, then the
-// wave's further chunks as in attention_kernel. Same tiles in the same order per
-// chunk: bit-identical to attention_kernel<64> (non-causal).
-template <typename T>
-__global__ __launch_bounds__(640) void attention_2p_kernel(const T* __restrict__ qkv,
-                                                           T* __restrict__ out, int N, int H,
-                                                           int Npad, int nchunks, float qk_scale,
-                                                           int prio) {
-  using G = HeadGeom<64>;
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  char* kimg = smem;
-  char* vimg = smem + Npad * G::ROWB;
-  const int bh = blockIdx.x;
-  const int b = bh / H, h = bh - b * H;
-  const int D = H * 64, ld = 3 * D;
-  const T* base = qkv + (size_t)b * N * ld + h * 64;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int nkt = Npad >> 5, TA = nkt / 2;
-  const float c2 = qk_scale * kLog2e;
-  const int c0 = wave;
-  i16x8 qf[G::NKS];
-  load_q<T, 64>(qf, base, ld, c0 < nchunks ? c0 : 0, N, lane);
-  asm volatile("s_waitcnt vmcnt(0)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
-  const int prow = lane >> 3, pch = lane & 7, pieces = Npad / 8, pa = TA * 4;
-  auto kv_piece = [&](bool isv, int piece) {
-    const int row = piece * 8 + prow;
-    const int r = row < N ? row : N - 1;
-    const int lch = isv ? (pch ^ ((row & 3) << 1)) : (pch ^ ((row >> 1) & 7));
-    glds16_hidden(base + (size_t)r * ld + (isv ? 2 * D : D) + lch * 8,
-                  (isv ? vimg : kimg) + piece * 1024);
-  };
-  const int nA = 2 * pa, nB = 2 * (pieces - pa), half = pieces - pa;
-  for (int pc = wave; pc < nA; pc += nw) kv_piece(pc >= pa, pc >= pa ? pc - pa : pc);
-  for (int pc = wave; pc < nB; pc += nw) kv_piece(pc >= half, pa + (pc >= half ? pc - half : pc));
-  wait_vm_upto(wave < nB ? (nB - wave + nw - 1) / nw : 0);   // this wave's phase A landed
-  __syncthreads();
-  f32x16 o[G::NDT];
-  float lsum = 0.f, m = 0.f;
-  if (c0 < nchunks)
-    attend_chunk<T, false, 64>(kimg, vimg, qf, c0, N, Npad, c2, lane, o, lsum, m, 0, TA, prio,
-                               true, false);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  T* obase = out + (size_t)b * N * D + h * 64;
-  if (c0 < nchunks) {
-    attend_chunk<T, false, 64>(kimg, vimg, qf, c0, N, Npad, c2, lane, o, lsum, m, TA, -1, prio,
-                               false, true);
-    attend_store<T, 64>(o, lsum, c0, N, obase, D, lane);
-  }
-  for (int chunk = c0 + nw; chunk < nchunks; chunk += nw) {
-    load_q<T, 64>(qf, base, ld, chunk, N, lane);
-    attend_chunk<T, false, 64>(kimg, vimg, qf, chunk, N, Npad, c2, lane, o, lsum, m, 0, -1,
-                               prio);
-    attend_store<T, 64>(o, lsum, chunk, N, obase, D, lane);
-  }
-}
-#endif  // MICLIP_EXPERIMENTS
 
 // ---------------------------------------------------------------------------
 // Pipelined form: one workgroup walks hpw consecutive (image, head) pairs.
@@ -930,319 +864,6 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
   MICLIP_STAMP_END(blockIdx.x * 8 + wave);
 }
 
-#ifdef MICLIP_EXPERIMENTS
-// Experimental (measured level with the x8 kernel): built only into
-// the diagnostic library (make exp), never into the product libmiclip.so.
-// ---------------------------------------------------------------------------
-// Streamed form of the x8 kernel (variant 9; N in 257..259, head dim 64). The
-// x8 kernel stages a head's whole K/V image (66 KiB) before any wave computes,
-// so a third of its wave time is the fetch of the next head (every CU fetching
-// at the chip's burst rate at once). Here the keys stream through a ring of R
-// 32-key slots (K tile 4 KiB + V tile 4 KiB) that runs on across the
-// workgroup's heads: at key tile g the DMA of tile g+R-1 is issued (one 1-KiB
-// piece per wave: waves 0-3 the K rows, 4-7 the V rows), so R-1 tiles are in
-// flight while the waves compute, and the next head's first tiles land under
-// this head's last ones. One counted vmcnt + one barrier per key tile.
-//   * Q: wave w's 32-query chunk is read into registers at the head's first
-//     tile; at its second tile the wave DMAs the next head's chunk into its
-//     private 4-KiB area (source-swizzled like K) and wave 0 the ragged rows
-//     256..263 into a 2 x 1 KiB head-parity area.
-//   * Full chunks: the x8 kernel's work in its order (attend_chunk per key tile
-//     0..7, the keys past 256 by attend_extra_keys): those rows equal the x8
-//     kernel's bit for bit.
-//   * The NR = N - 256 ragged queries run on VALU beside the stream instead of a
-//     31/32-masked MFMA chunk (which held 48 more VGPRs across the tile loop and
-//     spilled): at every tile wave w takes keys 4w..4w+3, lane (r = lane >> 4,
-//     dims 4 (lane & 15) ..+3) keeping an online-softmax state per (query, key
-//     row r); at the head's end the four row states fold into one partial per
-//     wave (LDS), and at the next head's first tile wave c merges query c's
-//     eight partials. Same arithmetic rules as the MFMA path (fp32 scores of
-//     exact products, base-2 exponentials, P rounded to the compute dtype for
-//     P.V, fp32 sums) in another summation order: these rows agree with the x8
-//     kernel's to rounding, not bitwise.
-//   * VM counter: every wave issues 1 tile DMA per position and 5 Q DMAs at a
-//     head's second tile (dummy 4-byte DMAs where it has fewer); the wait for
-//     tile g counts only those, so output stores issued since make it stricter,
-//     never looser.
-// LDS: R x 8 KiB + 32 KiB Q + 2 KiB ragged Q + partials; R = 5 (4 when N = 259)
-// ---------------------------------------------------------------------------
-// Sum over each 16-lane row, the same value on every lane of the row: four DPP
-// butterfly stages (half-mirror, mirror, quad xor 1, quad xor 2), each adding
-// a lane pair's two values in both lanes (a + b == b + a), so the row's lanes
-// stay identical stage by stage. VALU only (a __shfl_xor is an LDS round trip).
-MICLIP_DEV float row16_sum(float x) {
-  auto dpp = [](float v, int ctrl_sel) {
-    int r;
-    const int b = __float_as_int(v);
-    switch (ctrl_sel) {
-      case 0: r = __builtin_amdgcn_update_dpp(0, b, 0x141, 0xf, 0xf, false); break;  // row_half_mirror
-      case 1: r = __builtin_amdgcn_update_dpp(0, b, 0x140, 0xf, 0xf, false); break;  // row_mirror
-      case 2: r = __builtin_amdgcn_update_dpp(0, b, 0xB1, 0xf, 0xf, false); break;   // quad_perm 1,0,3,2
-      default: r = __builtin_amdgcn_update_dpp(0, b, 0x4E, 0xf, 0xf, false); break;  // quad_perm 2,3,0,1
-    }
-    return __int_as_float(r);
-  };
-  x += dpp(x, 0);
-  x += dpp(x, 1);
-  x += dpp(x, 2);
-  x += dpp(x, 3);
-  return x;
-}
-
-MICLIP_DEV void wait_vm(int n) {
-  switch (n) {
-#define MICLIP_VMC(k) \
-  case k:           \
-    asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-    MICLIP_VMC(0) MICLIP_VMC(1) MICLIP_VMC(2) MICLIP_VMC(3) MICLIP_VMC(4) MICLIP_VMC(5)
-    MICLIP_VMC(6) MICLIP_VMC(7) MICLIP_VMC(8) MICLIP_VMC(9) MICLIP_VMC(10) MICLIP_VMC(11)
-    MICLIP_VMC(12) MICLIP_VMC(13) MICLIP_VMC(14) MICLIP_VMC(15) MICLIP_VMC(16)
-#undef MICLIP_VMC
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-
-constexpr int kStreamTiles = 9;   // key tiles per head: 8 full + the rows past 256
-
-template <typename T, int NR, int R>
-__global__ __launch_bounds__(512, 4) void attention_stream_kernel(const T* __restrict__ qkv,
-                                                                 T* __restrict__ out, int B,
-                                                                 int N, int H, int Npad, int hpw,
-                                                                 float qk_scale, int prio) {
-  static_assert(NR >= 1 && NR <= 3, "1..3 ragged queries");
-  static_assert(R >= 3 && R <= 8, "ring depth: the Q batch of tile 1 must retire by the next head");
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  constexpr int SLOT = 8192;                   // K tile 4 KiB + V tile 4 KiB
-  char* qarea = smem + R * SLOT;               // [8 waves][32 rows][128 B]
-  char* qrag = qarea + 8 * 4096;               // [2 parities][8 rows][128 B]
-  float* part = (float*)(qrag + 2048);         // [NR queries][8 waves][66]
-  char* sink = (char*)(part + NR * 8 * 66);    // dummy-DMA target (never read)
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int D = H * 64, ld = 3 * D;
-  const float c2 = qk_scale * kLog2e;
-  const int bh0 = blockIdx.x * hpw;
-  const int nh = (B * H - bh0) < hpw ? (B * H - bh0) : hpw;
-  auto head_base = [&](int j) {
-    const int bh = bh0 + j, b = bh / H, h = bh - b * H;
-    return qkv + (size_t)b * N * ld + h * 64;
-  };
-  auto head_out = [&](int j) {
-    const int bh = bh0 + j, b = bh / H, h = bh - b * H;
-    return out + (size_t)b * N * D + h * 64;
-  };
-  // The lane-dependent parts of the DMA / LDS addresses are rebuilt at each use
-  // from an opaque copy of the lane id: hoisted out of the tile loop they were
-  // kept in VGPRs across it and spilled (and every scratch reload made hipcc
-  // wait vmcnt(0), draining the ring).
-  auto opaque_lane = [&]() {
-    int lo = lane;
-    asm volatile("" : "+v"(lo));
-    return lo;
-  };
-  // key tile kt of the head at `base` into ring slot `slot`: waves 0-3 K rows
-  // 8w.., 4-7 V rows 8(w-4)..; the partial ninth tile (rows 256..) has one K
-  // and one V piece (waves 0, 4). base == nullptr (no such head): a dummy op.
-  auto dma_tile = [&](const T* base, int kt, int slot) {
-    int w = wave;
-    asm volatile("" : "+s"(w));
-    const bool isv = w >= 4;
-    const int pw = w & 3;
-    if (base == nullptr || (kt == kStreamTiles - 1 && pw != 0)) {
-      glds4_hidden(qkv, sink);
-      return;
-    }
-    const int lo = opaque_lane();
-    const int row = 32 * kt + 8 * pw + (lo >> 3);
-    const int r = row < N ? row : N - 1;
-    const int lch = isv ? ((lo & 7) ^ ((row & 3) << 1)) : ((lo & 7) ^ ((row >> 1) & 7));
-    char* dst = smem + slot * SLOT + (isv ? 4096 : 0) + pw * 1024;
-    glds16_hidden(base + (size_t)r * ld + (isv ? 2 * D : D) + lch * 8, dst);
-  };
-  // head j's Q (base == nullptr: none): this wave's chunk (4 pieces) + (wave
-  // 0) the ragged rows into parity j & 1; always 5 ops
-  auto dma_q = [&](const T* base, int j) {
-    if (base == nullptr) {
-#pragma unroll
-      for (int p = 0; p < 5; ++p) glds4_hidden(qkv, sink);
-      return;
-    }
-    const int lo = opaque_lane();
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int row = 32 * wave + 8 * p + (lo >> 3);   // < 256 < N
-      glds16_hidden(base + (size_t)row * ld + (((lo & 7) ^ (row & 7)) << 3),
-                    qarea + wave * 4096 + p * 1024);
-    }
-    if (wave == 0) {
-      const int row = 256 + (lo >> 3), r = row < N ? row : N - 1;
-      glds16_hidden(base + (size_t)r * ld + (((lo & 7) ^ (row & 7)) << 3), qrag + (j & 1) * 1024);
-    } else {
-      glds4_hidden(qkv, sink);
-    }
-  };
-
-  // ragged queries: per (query q, key row r = lane >> 4) the running max, sum
-  // and O dims 4 (lane & 15) .. +3
-  float rm[NR], rl[NR], ro[NR][4];
-  u32x2 rq[NR];
-  // one key tile's keys 4w .. 4w+3 (row r per 16-lane group) for each query
-  auto ragged_tile = [&](const char* sk, const char* sv, int kt) {
-    const int lo = opaque_lane();
-    const int i = 4 * wave + (lo >> 4);           // key row in the tile
-    const int c = (lo & 15) >> 1;                 // 16-B chunk of dims 4 (lo & 15) ..
-    const u32x2 kv = *(const u32x2*)(sk + i * 128 + ((c ^ ((i >> 1) & 7)) << 4) + (lo & 1) * 8);
-    const u32x2 vv = *(const u32x2*)(sv + i * 128 + ((c ^ ((i & 3) << 1)) << 4) + (lo & 1) * 8);
-    const bool valid = kt < kStreamTiles - 1 || i < NR;   // ninth tile: keys 256 .. N-1
-    const i16x4 vh = __builtin_bit_cast(i16x4, vv);
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-      float sc = dot2acc<T>(rq[q][1], kv[1], dot2acc<T>(rq[q][0], kv[0], 0.f));
-      sc = row16_sum(sc);
-      sc = valid ? sc * c2 : -INFINITY;   // masked: al = 1, p = 0, an exact no-op
-      const float mn = fmaxf(rm[q], sc);
-      const float al = __builtin_amdgcn_exp2f(rm[q] - mn);
-      const float p = __builtin_amdgcn_exp2f(sc - mn);
-      rl[q] = rl[q] * al + p;
-      const float p16 = to_f<T>(to_t<T>(p));
-#pragma unroll
-      for (int e = 0; e < 4; ++e) ro[q][e] = ro[q][e] * al + p16 * from_bits<T>(vh[e]);
-      rm[q] = mn;
-      // the state is updated here, tile by tile: unpinned, hipcc sank the whole
-      // head's updates to its end, keeping every tile's scores and V rows live
-      // (and spilling them)
-      asm volatile("" : "+v"(rm[q]), "+v"(rl[q]), "+v"(ro[q][0]), "+v"(ro[q][1]), "+v"(ro[q][2]),
-                   "+v"(ro[q][3]));
-    }
-  };
-  // fold the four key-row states into this wave's partial of each query
-  auto ragged_fold = [&]() {
-    const int lo = opaque_lane();
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-      float mw = fmaxf(rm[q], __shfl_xor(rm[q], 16, 64));
-      mw = xor32_max(mw);
-      const float sc = __builtin_amdgcn_exp2f(rm[q] - mw);
-      float l = rl[q] * sc;
-      l += __shfl_xor(l, 16, 64);
-      l = xor32_sum(l);
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = ro[q][e] * sc;
-        v[e] += __shfl_xor(v[e], 16, 64);
-        v[e] = xor32_sum(v[e]);
-      }
-      float* pw = part + (q * 8 + wave) * 66;
-      if (lo < 16) {
-        *(f32x2*)(pw + 4 * lo) = f32x2{v[0], v[1]};
-        *(f32x2*)(pw + 4 * lo + 2) = f32x2{v[2], v[3]};
-      }
-      if (lo == 0) *(f32x2*)(pw + 64) = f32x2{mw, l};
-    }
-  };
-  // wave q < NR: query q's eight partials (published by a barrier since) -> row
-  // 256 + q of head j; lane = output dim
-  auto ragged_merge = [&](T* obase) {
-    if (wave >= NR) return;
-    const int lo = opaque_lane();
-    const float* pc = part + wave * 8 * 66;
-    float mx = pc[64];
-#pragma unroll
-    for (int w = 1; w < 8; ++w) mx = fmaxf(mx, pc[w * 66 + 64]);
-    float l = 0.f, acc = 0.f;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-      const float s = __builtin_amdgcn_exp2f(pc[w * 66 + 64] - mx);
-      l += s * pc[w * 66 + 65];
-      acc += s * pc[w * 66 + lo];
-    }
-    obase[(size_t)(256 + wave) * D + lo] = to_t<T>(acc / l);
-  };
-
-  // prologue: head 0's Q, then its tiles 0 .. R-2
-  const T* nbase = head_base(0);
-  dma_q(nbase, 0);
-#pragma unroll
-  for (int t = 0; t < R - 1; ++t) dma_tile(nbase, t, t);
-
-  f32x16 o[2];
-  float lsum = 0.f, m = 0.f;
-  i16x8 qf[4];
-  T* prev_out = nullptr;
-  int slot = 0;   // ring slot of the head's tile 0 (tile g lives in slot g % R)
-  for (int j = 0; j < nh; ++j) {
-    const T* base = nbase;
-    nbase = j + 1 < nh ? head_base(j + 1) : nullptr;
-    T* obase = head_out(j);
-    // the head's 9 key tiles, unrolled: every wait count, tile index and
-    // specialisation below is a constant (the loop's scalar bookkeeping was
-    // costing more issue slots than the per-tile MFMAs)
-#pragma unroll
-    for (int kt = 0; kt < kStreamTiles; ++kt) {
-      // tile landed: younger than its DMA are the R-2 tile DMAs issued after it
-      // and, at tiles 2 .. R, this head's Q batch (5 ops, issued at tile 1)
-      wait_vm(R - 2 + (kt >= 2 && kt <= R ? 5 : 0));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      int cur = slot + kt;
-      cur = cur >= R ? cur - R : cur;
-      cur = cur >= R ? cur - R : cur;
-      // tile kt+R-1 (this head's or the next one's) into the slot of tile kt-1:
-      // every wave is past it
-      const int prv = cur == 0 ? R - 1 : cur - 1;
-      if (kt + R - 1 < kStreamTiles)
-        dma_tile(base, kt + R - 1, prv);
-      else
-        dma_tile(nbase, kt + R - 1 - kStreamTiles, prv);
-      const char* sk = smem + cur * SLOT;
-      const char* sv = sk + 4096;
-      if (kt == 0) {
-        if (prev_out != nullptr) ragged_merge(prev_out);
-        // this head's Q: the chunk's fragments and the ragged rows, to registers
-        const int lo = opaque_lane();
-        const char* rows = qarea + wave * 4096;
-        const int r = lo & 31, hh = lo >> 5;
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2)
-          qf[s2] = *(const i16x8*)(rows + r * 128 + (((2 * s2 + hh) ^ (r & 7)) << 4));
-        const int c = (lo & 15) >> 1;
-#pragma unroll
-        for (int q = 0; q < NR; ++q) {
-          rq[q] = *(const u32x2*)(qrag + (j & 1) * 1024 + q * 128 + ((c ^ q) << 4) + (lo & 1) * 8);
-          rm[q] = -1e30f;
-          rl[q] = 0.f;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) ro[q][e] = 0.f;
-        }
-      }
-      if (kt == 1) dma_q(nbase, j + 1);   // the Q areas were read at tile 0 (lgkmcnt(0) above)
-      if (kt < kStreamTiles - 1) {
-        attend_chunk<T, false, 64, false>(sk, sv, qf, wave, N, Npad, c2, opaque_lane(), o, lsum,
-                                          m, 0, 1, prio, kt == 0, false);
-        ragged_tile(sk, sv, kt);
-      } else {
-        // the keys past the 8 full tiles (the partial ninth tile: rows 256 ..)
-        attend_extra_keys<T>(sk, sv, qf, o, lsum, m, 256, NR, c2, opaque_lane(), 256);
-        if (wave == 0) ragged_tile(sk, sv, kt);
-        ragged_fold();
-        lsum = xor32_sum(lsum);
-        attend_store<T, 64>(o, lsum, wave, N, obase, D, opaque_lane());
-      }
-    }
-    prev_out = obase;
-    slot += kStreamTiles;
-    slot %= R;
-  }
-  // the last head's ragged rows
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  ragged_merge(prev_out);
-  // nothing may land in LDS after the workgroup retires
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-#endif  // MICLIP_EXPERIMENTS
 
 // ---------------------------------------------------------------------------
 // One query per (image, head): token row 0 (CLS) only. The vision tower's last
@@ -1427,52 +1048,7 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, 
   // ragged one: K/V (72 KiB) plus the partials of 8 waves x the ragged queries
   // must stay under 80 KiB of LDS, i.e. N - 256 <= 3)
   const size_t lds_x8 = lds + (size_t)8 * (N > 256 ? N - 256 : 0) * 66 * 4;
-#ifdef MICLIP_EXPERIMENTS
-  if (variant == 9) {
-    // streamed x8 (attention_stream_kernel): N in 257..259, R key-tile slots
-    if (CAUSAL || N < 257 || N > 259) return hipErrorInvalidValue;
-    const int nr = N - 256;
-    const size_t fixed = 32768 + 2048 + (size_t)nr * 8 * 66 * 4 + 256;
-    const int R = 5 * 8192 + fixed <= 80 * 1024 ? 5 : 4;
-    // NR = 3 fits 4 slots in 80 KiB, NR 1-2 five
-    const void* kern = nr == 1 ? (const void*)attention_stream_kernel<T, 1, 5>
-                     : nr == 2 ? (const void*)attention_stream_kernel<T, 2, 5>
-                               : (const void*)attention_stream_kernel<T, 3, 4>;
-    if (R != (nr == 3 ? 4 : 5)) return hipErrorInvalidValue;
-    static bool st_attr[3] = {false, false, false};
-    if (!st_attr[nr - 1]) {
-      const hipError_t e =
-          hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-      if (e != hipSuccess) return e;
-      st_attr[nr - 1] = true;
-    }
-    static int ncu9 = [] {
-      int d = 0, n = 0;
-      if (hipGetDevice(&d) != hipSuccess ||
-          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
-        n = 256;
-      return n;
-    }();
-    const int heads = B * H, slots = 2 * ncu9;
-    int hpw = (heads + slots - 1) / slots;
-    hpw = hpw < 1 ? 1 : hpw;
-    const int grid = (heads + hpw - 1) / hpw;
-    const size_t lds = (size_t)R * 8192 + fixed;
-    const T* q = (const T*)qkv;
-    T* o = (T*)out;
-    if (nr == 1)
-      hipLaunchKernelGGL((attention_stream_kernel<T, 1, 5>), dim3(grid), dim3(512), lds, s, q, o,
-                         B, N, H, Npad, hpw, 0.125f, attn_prio());
-    else if (nr == 2)
-      hipLaunchKernelGGL((attention_stream_kernel<T, 2, 5>), dim3(grid), dim3(512), lds, s, q, o,
-                         B, N, H, Npad, hpw, 0.125f, attn_prio());
-    else
-      hipLaunchKernelGGL((attention_stream_kernel<T, 3, 4>), dim3(grid), dim3(512), lds, s, q, o,
-                         B, N, H, Npad, hpw, 0.125f, attn_prio());
-    return hipGetLastError();
-  }
-#endif  // MICLIP_EXPERIMENTS
-  if (variant == 9) return hipErrorInvalidValue;   // experiments build only
+  if (variant == 9) return hipErrorInvalidValue;   // removed (measured level)
   if (variant == 8 || (!CAUSAL && variant == 0 && N >= 256 && N < 288 && lds_x8 <= 80 * 1024)) {
     // at most 3 ragged queries: one per merging wave (attention_x8_kernel)
     if (CAUSAL || N < 256 || N > 259 || lds_x8 > 80 * 1024) return hipErrorInvalidValue;
@@ -1540,23 +1116,6 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, 
                          attn_prio());
     return hipGetLastError();
   }
-#ifdef MICLIP_EXPERIMENTS
-  // variant 3: the two-phase one-head-per-workgroup kernel (experiments library)
-  if (!CAUSAL && variant == 3 && nchunks >= 4 && lds <= 160 * 1024) {
-    static bool a2p = false;
-    if (!a2p) {
-      const hipError_t e = hipFuncSetAttribute((const void*)attention_2p_kernel<T>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               160 * 1024);
-      if (e != hipSuccess) return e;
-      a2p = true;
-    }
-    const int per = (nchunks + 9) / 10, nw = (nchunks + per - 1) / per;
-    hipLaunchKernelGGL((attention_2p_kernel<T>), dim3(B * H), dim3(nw * 64), lds, s,
-                       (const T*)qkv, (T*)out, N, H, Npad, nchunks, 0.125f, attn_prio());
-    return hipGetLastError();
-  }
-#endif  // MICLIP_EXPERIMENTS
   if (variant == 3) return hipErrorInvalidValue;
   return attn_launch_plain<T, CAUSAL, 64>(qkv, out, B, N, H, s, variant >= 10 ? variant : 0);
 }

@@ -1075,7 +1075,10 @@ int64_t miclip_model_bytes(const miclip_model* m) { return m ? m->bytes : 0; }
 
 int miclip_model_flags(const miclip_model* m) {
   if (!m) return 0;
-  return (m->resid16 ? MICLIP_MODEL_RESID16 : 0) | (m->lnfold ? MICLIP_MODEL_LNFOLD : 0) |
+  // ensure_folded skips the MX vision tower: LNFOLD names the vision tower only
+  return (m->resid16 ? MICLIP_MODEL_RESID16 : 0) |
+         (m->lnfold && !m->mx ? MICLIP_MODEL_LNFOLD : 0) |
+         (m->lnfold ? MICLIP_MODEL_LNFOLD_TEXT : 0) |
          (m->mx ? MICLIP_MODEL_MXFP8 : 0) | (m->cls_last ? MICLIP_MODEL_CLS_LAST : 0) |
          (m->mx_out ? MICLIP_MODEL_MX_OUT : 0) |
          (m->mx && !m->mx_gelu_erf ? MICLIP_MODEL_MX_GELU_TANH : 0);
@@ -1089,13 +1092,8 @@ int miclip_set_gemm_variant(miclip_model* m, int32_t which, int32_t variant) {
     m->gemm_variant[2] = variant;
     return 0;
   }
-#ifdef MICLIP_EXPERIMENTS
-  if (variant != 0 && variant != 259 && variant != 508 && variant != 516)
-    return fail(MICLIP_EINVAL, "gemm variant must be 0, 259, 508 or 516 (bit-identical kernels)");
-#else
   if (variant != 0 && variant != 259)
-    return fail(MICLIP_EINVAL, "gemm variant must be 0 or 259 (508 / 516: experiments library)");
-#endif
+    return fail(MICLIP_EINVAL, "gemm variant must be 0 or 259");
   m->gemm_variant[which] = variant;
   return 0;
 }
@@ -1125,6 +1123,27 @@ int miclip_op_gemm(int32_t dtype, const void* A, const void* W, const float* bia
   } else if (epi == 4) {
     if (!bias) return fail(MICLIP_EINVAL, "residual epilogue needs a bias");
     MICLIP_HIP(gemm_residual(dtype, A, W, bias, C, M, N, K, s, variant, 1));
+  } else {
+    return fail(MICLIP_EINVAL, "unknown epilogue");
+  }
+  return 0;
+}
+
+int miclip_op_gemm_splitk(int32_t dtype, const void* A, const void* W, const float* bias,
+                          const float* c, const float* colsum, const float* stats, void* C,
+                          int32_t M, int32_t N, int32_t K, int32_t epi, int32_t act, int32_t sk,
+                          float* ws, void* stream) {
+  if (!A || !W || !C || !ws) return fail(MICLIP_EINVAL, "null argument");
+  if (sk < 2 || sk > 64) return fail(MICLIP_EINVAL, "sk must be in 2..64");
+  hipStream_t s = (hipStream_t)stream;
+  if (epi == 0) {
+    MICLIP_HIP(gemm_store(dtype, A, W, bias, C, M, N, K, act, s, 0, ws, sk));
+  } else if (epi == 1 || epi == 4) {
+    if (!bias) return fail(MICLIP_EINVAL, "residual epilogue needs a bias");
+    MICLIP_HIP(gemm_residual(dtype, A, W, bias, C, M, N, K, s, 0, epi == 4, ws, sk));
+  } else if (epi == 5) {
+    if (!c || !colsum || !stats) return fail(MICLIP_EINVAL, "folded-LN epilogue needs c, colsum, stats");
+    MICLIP_HIP(gemm_store_ln(dtype, A, W, c, colsum, stats, C, M, N, K, act, s, 0, ws, sk));
   } else {
     return fail(MICLIP_EINVAL, "unknown epilogue");
   }

@@ -8,7 +8,8 @@
 //                x @ visual.proj: fp32 on the f32-input MFMA (head_proj_kernel)
 //   zero_shot    x @ visual.proj -> F.normalize -> scale * f @ text_weights -> topk
 //                (methods/ProLIP.py:38-41, 288-293; methods/utils.py:16-21), fp32:
-//                head_proj_kernel, then head_logits_kernel (one workgroup per row)
+//                head_proj_kernel, head_logits_kernel (f32 MFMA, normalise fused),
+//                topk_rows_kernel
 // All of these are small next to the transformer blocks.
 #include "common.h"
 #include "kernels.h"
@@ -102,16 +103,59 @@ __global__ __launch_bounds__(64) void eot_kernel(const int64_t* __restrict__ tok
   if (lane == 0) eot_rows[p] = p * L + bi;
 }
 
-// out[b, e] = sum_d x[b, d] * W[d, e] in fp32 on the f32-input MFMA
-// (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32 accumulation; the
-// projection of methods/ProLIP.py:38-41 / clip/model.py:335 and 352). One
-// workgroup = 16 rows x 16 columns; its 4 waves take d in quarters, each a chain
-// of MFMAs, and the 4 partial tiles are summed in a fixed order through LDS
-// (deterministic, batch-invariant: a row's result does not depend on B).
-// Per 16-k step lane (g = lane >> 4, i = lane & 15) loads x[row i][d + 4g .. +3]
-// as one float4 and W[d + 4g + s][col i] for s = 0..3; MFMA s then multiplies the
-// k = d + 4g + s pairs (the same k permutation on both operands). Grid
-// (ceil(B/16), ceil(E/16)): 768 workgroups at B = 256, E = 768. Din % 64 == 0.
+// One wave's share of a 16 x 16 fp32 product on the f32-input MFMA
+// (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32 accumulation): the sum over
+// k chunks [c0, c1) of 16 k each of x[row][k] * W[k][col]. Lane (i = lane & 15,
+// g = lane >> 4) loads x[row i][16 ch + 4g .. +3] as one float4 (xp = row i + 4g)
+// and W[16 ch + 4g + s][col i] for s = 0..3 (wp = W + 4g * ldw + col i); MFMA s
+// multiplies the k = 16 ch + 4g + s pairs (the same k permutation on both
+// operands), chunks in ascending order. NORM: n2 += the squares of the lane's x
+// elements (a row's |x|^2 in the same loop, for the fused normalise).
+template <bool NORM>
+__device__ __forceinline__ f32x4 mfma_chunks(const float* __restrict__ xp,
+                                             const float* __restrict__ wp, size_t ldw, int c0,
+                                             int c1, float& n2) {
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  int ch = c0;
+  for (; ch + 4 <= c1; ch += 4) {
+    float4 a[4];
+    float bv[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a[u] = *(const float4*)(xp + 16 * (ch + u));
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) bv[u][s2] = wp[(size_t)(16 * (ch + u) + s2) * ldw];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].x, bv[u][0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].y, bv[u][1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].z, bv[u][2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].w, bv[u][3], acc, 0, 0, 0);
+      if (NORM)
+        n2 = fmaf(a[u].w, a[u].w, fmaf(a[u].z, a[u].z, fmaf(a[u].y, a[u].y, fmaf(a[u].x, a[u].x, n2))));
+    }
+  }
+  for (; ch < c1; ++ch) {
+    const float4 a = *(const float4*)(xp + 16 * ch);
+    float bv[4];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) bv[s2] = wp[(size_t)(16 * ch + s2) * ldw];
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bv[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bv[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bv[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bv[3], acc, 0, 0, 0);
+    if (NORM) n2 = fmaf(a.w, a.w, fmaf(a.z, a.z, fmaf(a.y, a.y, fmaf(a.x, a.x, n2))));
+  }
+  return acc;
+}
+
+// out[b, e] = sum_d x[b, d] * W[d, e] in fp32 on the f32 MFMA (the projection of
+// methods/ProLIP.py:38-41 / clip/model.py:335 and 352). One workgroup = 16 rows x
+// 16 columns; wave w takes k chunks [w nk / 4, (w + 1) nk / 4) of the nk = Din / 16,
+// and the 4 partial tiles are summed in a fixed order through LDS (deterministic,
+// batch-invariant: a row's result does not depend on B). Grid (ceil(B/16),
+// ceil(E/16)): 768 workgroups at B = 256, E = 768. Din % 16 == 0.
 __global__ __launch_bounds__(256) void head_proj_kernel(const float* __restrict__ x,
                                                         const float* __restrict__ W,
                                                         float* __restrict__ out, int B, int Din,
@@ -120,27 +164,10 @@ __global__ __launch_bounds__(256) void head_proj_kernel(const float* __restrict_
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
   const int b0 = blockIdx.x * 16, c0 = blockIdx.y * 16;
   const int row = b0 + i < B ? b0 + i : B - 1, col = c0 + i < E ? c0 + i : E - 1;
-  const int q = Din / 4, d0 = w * q;
-  const float* xp = x + (size_t)row * Din + d0 + 4 * g;
-  const float* wp = W + (size_t)(d0 + 4 * g) * E + col;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int d = 0; d < q; d += 64) {
-    float4 a[4];
-    float bv[4][4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      a[u] = *(const float4*)(xp + d + 16 * u);
-#pragma unroll
-      for (int s2 = 0; s2 < 4; ++s2) bv[u][s2] = wp[(size_t)(d + 16 * u + s2) * E];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].x, bv[u][0], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].y, bv[u][1], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].z, bv[u][2], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].w, bv[u][3], acc, 0, 0, 0);
-    }
-  }
+  const int nk = Din / 16;
+  float n2 = 0.f;
+  const f32x4 acc = mfma_chunks<false>(x + (size_t)row * Din + 4 * g, W + (size_t)(4 * g) * E + col,
+                                       E, w * nk / 4, (w + 1) * nk / 4, n2);
   if (w > 0) red[w - 1][lane] = acc;
   __syncthreads();
   if (w > 0) return;
@@ -154,68 +181,62 @@ __global__ __launch_bounds__(256) void head_proj_kernel(const float* __restrict_
   }
 }
 
-// The zero-shot head on projected rows f [B, E] (methods/ProLIP.py:288-291,
-// methods/utils.py:16-21): logits = scale * F.normalize(f) @ tw [E, C], then
-// the top-k classes (largest first, ties -> lower index). One workgroup per row:
-// the 4 waves sum |f|^2 (fixed order); then for each chunk of 16 classes every
-// thread takes rows e = tid, tid + 256, ... of tw (16 contiguous floats each,
-// all loads in flight at once), and each class's 256 partials are summed by a
-// wave reduction and the 4 waves in a fixed order; wave 0 selects the top-k by
-// k wave-wide arg-max reductions over the logits staged in LDS.
+// The zero-shot logits on the f32 MFMA with the normalise fused (methods/ProLIP.py:
+// 288-291, methods/utils.py:16-21): logits[b, c] = scale * (f[b] . tw[:, c]) /
+// max(|f[b]|, 1e-12) for f [B, E], tw [E, C]. The tile is head_proj_kernel's (16
+// rows x 16 classes, 4 waves over k quarters, fixed-order LDS sum); each lane also
+// sums the squares of the f elements it loads for the MFMA, so |f[b]|^2 comes out
+// of the same loop (lane groups g in a fixed butterfly, then the 4 waves in a
+// fixed order): f is read once, no normalised copy is written. Grid (ceil(B/16),
+// ceil(C/16)): 16 x 63 workgroups at B = 256, C = 1000. E % 16 == 0.
 __global__ __launch_bounds__(256) void head_logits_kernel(const float* __restrict__ f,
                                                           const float* __restrict__ tw,
-                                                          float* __restrict__ logits,
-                                                          int32_t* __restrict__ topk, int E,
-                                                          int C, float scale, int k) {
-  constexpr int CC = 16;
-  extern __shared__ float sm[];
-  float* fs = sm;              // [E] the row, normalised
-  float* ls = fs + E;          // [C] logits
-  __shared__ float red[4][CC];
-  __shared__ float nred[4];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const float* fr = f + (size_t)blockIdx.x * E;
+                                                          float* __restrict__ logits, int B,
+                                                          int E, int C, float scale) {
+  __shared__ f32x4 red[3][64];
+  __shared__ float nred[4][16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 15, g = lane >> 4;
+  const int b0 = blockIdx.x * 16, c0 = blockIdx.y * 16;
+  const int row = b0 + i < B ? b0 + i : B - 1, col = c0 + i < C ? c0 + i : C - 1;
+  const int nk = E / 16;
   float n2 = 0.f;
-  for (int e = tid; e < E; e += 256) {
-    const float v = fr[e];
-    fs[e] = v;
-    n2 = fmaf(v, v, n2);
-  }
-  n2 = wave_sum(n2);
-  if (lane == 0) nred[w] = n2;
+  const f32x4 acc = mfma_chunks<true>(f + (size_t)row * E + 4 * g, tw + (size_t)(4 * g) * C + col,
+                                      C, w * nk / 4, (w + 1) * nk / 4, n2);
+  n2 += __shfl_xor(n2, 16);   // (g0 + g1) + (g2 + g3) on every lane of row i
+  n2 += __shfl_xor(n2, 32);
+  if (g == 0) nred[w][i] = n2;
+  if (w > 0) red[w - 1][lane] = acc;
   __syncthreads();
-  const float inv = 1.0f / fmaxf(sqrtf((nred[0] + nred[1]) + (nred[2] + nred[3])), 1e-12f);
-  for (int c0 = 0; c0 < C; c0 += CC) {
-    const int cc = C - c0 < CC ? C - c0 : CC;
-    float acc[CC];
+  if (w > 0) return;
+  const f32x4 r1 = red[0][lane], r2 = red[1][lane], r3 = red[2][lane];
 #pragma unroll
-    for (int c = 0; c < CC; ++c) acc[c] = 0.f;
-    for (int e = tid; e < E; e += 256) {
-      const float fe = fs[e] * inv;
-      const float* tr = tw + (size_t)e * C + c0;
-#pragma unroll
-      for (int c = 0; c < CC; ++c) acc[c] = fmaf(fe, tr[c < cc ? c : cc - 1], acc[c]);
-    }
-#pragma unroll
-    for (int c = 0; c < CC; ++c) {
-      const float v = wave_sum(acc[c]);
-      if (lane == 0) red[w][c] = v;
-    }
-    __syncthreads();
-    if (tid < cc) {
-      const float v = scale * ((red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]));
-      ls[c0 + tid] = v;
-      logits[(size_t)blockIdx.x * C + c0 + tid] = v;
-    }
-    __syncthreads();
+  for (int j = 0; j < 4; ++j) {
+    const int rl = 4 * g + j, r = b0 + rl;
+    const float nn = (nred[0][rl] + nred[1][rl]) + (nred[2][rl] + nred[3][rl]);
+    const float inv = 1.0f / fmaxf(sqrtf(nn), 1e-12f);
+    if (r < B && c0 + i < C)
+      logits[(size_t)r * C + c0 + i] = scale * (((acc[j] + r1[j]) + (r2[j] + r3[j])) * inv);
   }
-  if (!topk || w != 0) return;
+}
+
+// The top-k classes of each logits row (largest first, ties -> lower index; the
+// order torch.topk(sorted=True) returns for distinct values), one wave per row:
+// pick j is the arg-max over the classes strictly after pick j - 1 in (value
+// descending, index ascending) order, so no state but the previous pick is kept
+// and the row (L2-resident, C floats) is re-read per pick.
+__global__ __launch_bounds__(64) void topk_rows_kernel(const float* __restrict__ logits,
+                                                       int32_t* __restrict__ topk, int C, int k) {
+  const int lane = threadIdx.x;
+  const float* lr = logits + (size_t)blockIdx.x * C;
+  float pv = INFINITY;
+  int pi = -1;
   for (int j = 0; j < k; ++j) {
     float bv = -INFINITY;
     int bi = C;
     for (int c = lane; c < C; c += 64) {
-      const float v = ls[c];
-      if (bi == C || v > bv) { bv = v; bi = c; }   // ascending c: ties keep the lower index
+      const float v = lr[c];
+      const bool after = v < pv || (v == pv && c > pi);
+      if (after && (bi == C || v > bv)) { bv = v; bi = c; }   // ascending c: ties keep the lower
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -223,13 +244,9 @@ __global__ __launch_bounds__(256) void head_logits_kernel(const float* __restric
       const int oi = __shfl_xor(bi, o);
       if (oi < C && (bi == C || ov > bv || (ov == bv && oi < bi))) { bv = ov; bi = oi; }
     }
-    if (lane == 0) {
-      topk[(size_t)blockIdx.x * k + j] = bi;
-      ls[bi] = -INFINITY;
-    }
-    // one wave left: its LDS ops are in order; keep the compiler from moving
-    // the next scan's reads above lane 0's write
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) topk[(size_t)blockIdx.x * k + j] = bi;
+    pv = bv;
+    pi = bi;
   }
 }
 
@@ -357,7 +374,7 @@ hipError_t token_embed(const int64_t* tokens, const float* tok_emb, const float*
 
 hipError_t rowvec_matmul(const float* in, const float* Wm, float* out, int R, int D, int E,
                          hipStream_t s) {
-  if (R < 1 || D < 64 || D % 64 || E < 1) return hipErrorInvalidValue;
+  if (R < 1 || D < 16 || D % 16 || E < 1) return hipErrorInvalidValue;
   hipLaunchKernelGGL(head_proj_kernel, dim3((R + 15) / 16, (E + 15) / 16), dim3(256), 0, s, in,
                      Wm, out, R, D, E);
   return hipGetLastError();
@@ -366,17 +383,18 @@ hipError_t rowvec_matmul(const float* in, const float* Wm, float* out, int R, in
 hipError_t zero_shot(const float* x, const float* proj, const float* tw, float* logits,
                      int32_t* topk, int B, int Din, int E, int C, float scale, int k,
                      hipStream_t s, float* scratch) {
-  if (B < 1 || C < 1 || E < 1 || k < 0 || k > C || (!proj && Din != E) || (proj && !scratch))
+  if (B < 1 || C < 1 || E < 16 || E % 16 || k < 0 || k > C || (!proj && Din != E) ||
+      (proj && !scratch))
     return hipErrorInvalidValue;
-  const size_t lds = (size_t)(E + C) * sizeof(float);
-  if (lds > 64 * 1024) return hipErrorInvalidValue;
   if (proj) {
-    // the projection on the f32 MFMA over the whole chip, then the head per row
+    // the projection on the f32 MFMA over the whole chip, then the logits
     if (hipError_t e = rowvec_matmul(x, proj, scratch, B, Din, E, s)) return e;
     x = scratch;
   }
-  hipLaunchKernelGGL(head_logits_kernel, dim3(B), dim3(256), lds, s, x, tw, logits, topk, E, C,
-                     scale, k);
+  hipLaunchKernelGGL(head_logits_kernel, dim3((B + 15) / 16, (C + 15) / 16), dim3(256), 0, s, x,
+                     tw, logits, B, E, C, scale);
+  if (topk && k > 0)
+    hipLaunchKernelGGL(topk_rows_kernel, dim3(B), dim3(64), 0, s, logits, topk, C, k);
   return hipGetLastError();
 }
 

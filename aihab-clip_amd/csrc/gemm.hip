@@ -1436,362 +1436,6 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
   MICLIP_STAMP_END(blockIdx.x * 8 + wave);
 }
 
-#ifdef MICLIP_EXPERIMENTS
-// Experimental kernels (measured slower than the defaults): built
-// only into the diagnostic library (make exp -> build/exp/libmiclip_exp.so), never
-// into the product libmiclip.so.
-// ---------------------------------------------------------------------------
-// gemm4s: 256x256 tiles, 256 threads = 4 waves (2 x 2), 128 x 128 outputs per
-// wave -- ONE wave per SIMD with the 512-register budget: its 8 x 8 grid of
-// 16x16 fp32 accumulators in the AGPR half (the MFMAs are issued from inline asm
-// on "a" operands, so hipcc never moves an accumulator through VGPRs), plus two
-// sets of 16 fragments in VGPRs (the 32-k step being multiplied and the next).
-// The 8-wave kernel (gemm256s_kernel) alternates a compute segment of 16 MFMAs
-// with a load segment (fragment reads, 2 LDS-DMA pieces, a wait, a barrier)
-// between the two waves of a SIMD, and the load segment often outlasts the
-// partner's MFMAs. Here each wave feeds its own matrix pipe:
-// per 32-k step it issues 64 MFMAs and, between them, the 16 fragment reads of the
-// NEXT step (half the LDS bytes per MFMA of the 128 x 64 layout) and its share of
-// the LDS-DMA, with one counted wait + barrier per 64-k K-tile.
-//   * LDS: two stages of 64 KiB (A 256 rows | W 256 rows, 128-B rows = 64 k) with
-//     the 16-B chunk XOR swizzle chunk ^ (row & 7) on the DMA source and on the
-//     read (conflict-free ds_read_b128, as in gemm256s_kernel), and 2 x 4 KiB of
-//     epilogue operands (bias, column sums, row statistics) by tile parity.
-//   * Pipeline over k-steps (two per K-tile G, stage G & 1): the odd step 2G+1
-//     opens with vmcnt(0) + barrier (K-tile G+1 has landed in every wave's view,
-//     and no wave reads stage G & 1 again), reads K-tile G+1's first fragments
-//     while it multiplies, and issues the first DODD of the 16 DMA pieces of
-//     K-tile G+2 into stage G & 1; the even step 2G+2 issues the rest. A DMA
-//     cursor walks the K-tiles of this workgroup's tiles in order (past the last
-//     one it re-fetches the last K-tile into stages nobody reads again, so the
-//     steps stay branch-free). The DMAs are inline asm (hidden from hipcc's
-//     waitcnt pass), so the counted waits are the only ones.
-//   * Persistent over full 256-row tiles: one workgroup per CU walks tiles
-//     blockIdx.x + k * grid in the XCD-grouped order of gemm256s_kernel, and the
-//     stage pipeline runs straight across tile boundaries (the next tile's
-//     K-tile 0 and first fragments are in flight during this tile's epilogue).
-//     Rows past the last full tile-row are row-tail tasks on the same
-//     workgroups (gemm_tail_wg<NW = 4>).
-//   * Epilogue from registers, no LDS staging (both stages stay busy): the MFMA
-//     operands are swapped (C^T = W . A^T), so a lane holds 4 consecutive columns
-//     of one output row per 16x16 block; val4 / val4ln (the functors' exact
-//     operations) convert in registers, one v_permlane16_swap per dword pairs two
-//     blocks so that every lane holds 8 consecutive columns, and each 16-B store
-//     writes 64 contiguous bytes of 16 rows. Same k order and functors as every
-//     other path: outputs bit-identical to gemm256s_kernel and the tail tasks.
-// ---------------------------------------------------------------------------
-// The 256 accumulators live in a0..a255 by hand: every MFMA is an inline-asm
-// statement naming its accumulator registers literally and clobbering the whole
-// AGPR file, so hipcc never holds a value of its own in an AGPR across one and
-// never sees the accumulators as values (given them as C++ values it copied all
-// 256 out at the K-loop exit and spilled ~130 VGPRs). Audit after every edit:
-// `make asm` and require no compiler v_accvgpr_* / scratch in gemm4s_kernel
-// (tests/test_asm_hazards.py checks it). Accumulator (i, j) of the 8 x 8 grid
-// is a[4(8i+j) .. 4(8i+j)+3]. The asm MFMAs are opaque to hipcc's hazard
-// recognizer: the epilogue opens with 16 wait states before its first read.
-#define MICLIP_AGPR_CLOBBERS \
-  "a0", "a1", "a2", "a3", "a4", "a5", "a6", "a7", "a8", "a9", "a10", "a11", "a12", "a13", "a14", "a15", \
-  "a16", "a17", "a18", "a19", "a20", "a21", "a22", "a23", "a24", "a25", "a26", "a27", "a28", "a29", "a30", "a31", \
-  "a32", "a33", "a34", "a35", "a36", "a37", "a38", "a39", "a40", "a41", "a42", "a43", "a44", "a45", "a46", "a47", \
-  "a48", "a49", "a50", "a51", "a52", "a53", "a54", "a55", "a56", "a57", "a58", "a59", "a60", "a61", "a62", "a63", \
-  "a64", "a65", "a66", "a67", "a68", "a69", "a70", "a71", "a72", "a73", "a74", "a75", "a76", "a77", "a78", "a79", \
-  "a80", "a81", "a82", "a83", "a84", "a85", "a86", "a87", "a88", "a89", "a90", "a91", "a92", "a93", "a94", "a95", \
-  "a96", "a97", "a98", "a99", "a100", "a101", "a102", "a103", "a104", "a105", "a106", "a107", "a108", "a109", "a110", "a111", \
-  "a112", "a113", "a114", "a115", "a116", "a117", "a118", "a119", "a120", "a121", "a122", "a123", "a124", "a125", "a126", "a127", \
-  "a128", "a129", "a130", "a131", "a132", "a133", "a134", "a135", "a136", "a137", "a138", "a139", "a140", "a141", "a142", "a143", \
-  "a144", "a145", "a146", "a147", "a148", "a149", "a150", "a151", "a152", "a153", "a154", "a155", "a156", "a157", "a158", "a159", \
-  "a160", "a161", "a162", "a163", "a164", "a165", "a166", "a167", "a168", "a169", "a170", "a171", "a172", "a173", "a174", "a175", \
-  "a176", "a177", "a178", "a179", "a180", "a181", "a182", "a183", "a184", "a185", "a186", "a187", "a188", "a189", "a190", "a191", \
-  "a192", "a193", "a194", "a195", "a196", "a197", "a198", "a199", "a200", "a201", "a202", "a203", "a204", "a205", "a206", "a207", \
-  "a208", "a209", "a210", "a211", "a212", "a213", "a214", "a215", "a216", "a217", "a218", "a219", "a220", "a221", "a222", "a223", \
-  "a224", "a225", "a226", "a227", "a228", "a229", "a230", "a231", "a232", "a233", "a234", "a235", "a236", "a237", "a238", "a239", \
-  "a240", "a241", "a242", "a243", "a244", "a245", "a246", "a247", "a248", "a249", "a250", "a251", "a252", "a253", "a254", "a255"
-
-template <int N, class F, int... I>
-MICLIP_DEV void static_for_impl(F& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, class F>
-MICLIP_DEV void static_for(F&& f) {
-  static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
-}
-
-// acc[A] += W-fragment . A-fragment^T (operands swapped: C^T = W . A^T); ZERO: C = 0
-template <typename T, int A, bool ZERO>
-MICLIP_DEV void mfma_acc(const i16x8& w, const i16x8& a) {
-  if constexpr (std::is_same_v<T, _Float16>) {
-    if constexpr (ZERO)
-      asm volatile("v_mfma_f32_16x16x32_f16 a[%c2:%c3], %0, %1, 0"
-                   :: "v"(w), "v"(a), "i"(4 * A), "i"(4 * A + 3) : "memory", MICLIP_AGPR_CLOBBERS);
-    else
-      asm volatile("v_mfma_f32_16x16x32_f16 a[%c2:%c3], %0, %1, a[%c2:%c3]"
-                   :: "v"(w), "v"(a), "i"(4 * A), "i"(4 * A + 3) : "memory", MICLIP_AGPR_CLOBBERS);
-  } else {
-    if constexpr (ZERO)
-      asm volatile("v_mfma_f32_16x16x32_bf16 a[%c2:%c3], %0, %1, 0"
-                   :: "v"(w), "v"(a), "i"(4 * A), "i"(4 * A + 3) : "memory", MICLIP_AGPR_CLOBBERS);
-    else
-      asm volatile("v_mfma_f32_16x16x32_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]"
-                   :: "v"(w), "v"(a), "i"(4 * A), "i"(4 * A + 3) : "memory", MICLIP_AGPR_CLOBBERS);
-  }
-}
-// accumulator A into VGPRs (the epilogue)
-template <int A>
-MICLIP_DEV float4 acc_read() {
-  float x, y, z, w;
-  asm volatile(
-      "v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\t"
-      "v_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
-      : "=v"(x), "=v"(y), "=v"(z), "=v"(w)
-      : "i"(4 * A), "i"(4 * A + 1), "i"(4 * A + 2), "i"(4 * A + 3));
-  return make_float4(x, y, z, w);
-}
-
-// DIAG (diagnostic builds, outputs meaningless): 1 = no LDS-DMA after the
-// prologue (the main loop multiplies stale stages), 2 = the epilogue computes but
-// stores nothing. They price the DMA issue and the epilogue stores.
-// DODD of a K-tile's 16 DMA pieces go out in the odd step (spread over its 8
-// MFMA rows), the other 16 - DODD in the even step, spread over its first EROWS
-// rows (they must land before the next odd step's wait)
-template <typename T, class Epi, int DODD = 8, int DIAG = 0, int EROWS = 4>
-__global__ __launch_bounds__(256, 1) void gemm4s_kernel(const T* __restrict__ A,
-                                                        const T* __restrict__ W, int M, int N,
-                                                        int K, Epi epi, int gm, int ntm_dp,
-                                                        int ntail, int tail_wide) {
-  static_assert(TrAcc<Epi>::value, "gemm4s: transposed-accumulator epilogues only");
-  static_assert(DODD >= 0 && DODD <= 16 && EROWS >= 1 && EROWS <= 8, "DMA split");
-  constexpr int PE = 16 - DODD;   // pieces in the even step
-  // pieces of row r: [lo(r), lo(r + 1)) of P spread over R rows
-  constexpr auto lo = [](int r, int P, int R) { return r >= R ? P : (r * P + R - 1) / R; };
-  constexpr bool LN = IsLN<Epi>::value;
-  constexpr bool RES = PrefetchX<Epi>::value;   // fp16 residual stream: x + t at the store
-  constexpr int STAGE = 65536, WOFF = 32768, OPS = 2 * STAGE;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 8192];
-  const int ntn = N / 256, ndp = ntm_dp * ntn, nk = K / 64;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-  const int fr = lane & 15, fk = lane >> 4;
-  // DMA piece = 8 rows x 128 B; lane -> row lane >> 3, source chunk (lane & 7) ^ (lane >> 3)
-  const int prow = lane >> 3, pch = (lane & 7) ^ prow;
-  // fragment reads: row (block base) + fr, logical 16-B chunk 4h + fk
-  const int aoff0 = (wr * 128 + fr) * 128 + (((0 + fk) ^ (fr & 7)) << 4);
-  const int aoff1 = (wr * 128 + fr) * 128 + (((4 + fk) ^ (fr & 7)) << 4);
-  const int boff0 = WOFF + (wc * 128 + fr) * 128 + (((0 + fk) ^ (fr & 7)) << 4);
-  const int boff1 = WOFF + (wc * 128 + fr) * 128 + (((4 + fk) ^ (fr & 7)) << 4);
-  const size_t pstride = (size_t)8 * K;   // elements between the rows of two pieces
-
-  auto tile_of = [&](int id, int& m0_, int& n0_) {
-    int tm_, tn_;
-    group_tile(xcd_remap(id, ndp), ntm_dp, ntn, gm, tm_, tn_);
-    m0_ = tm_ * 256;
-    n0_ = tn_ * 256;
-  };
-  const int ntiles =
-      ndp > (int)blockIdx.x ? (ndp - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-
-  // DMA cursor: the next K-tile to fetch (tile index f_ti of this workgroup, K-tile
-  // f_kt); fa / fw = this lane's source of A / W piece 0 (wave w issues A pieces
-  // 8w..8w+7 = rows m0 + 64w + 8q + prow, and the W pieces likewise)
-  int f_ti = 0, f_kt = 0;
-  const T* fa_p = A;
-  const T* fw_p = W;
-  auto cursor_tile = [&](int ti) {
-    int m0_, n0_;
-    tile_of((int)blockIdx.x + ti * (int)gridDim.x, m0_, n0_);
-    fa_p = A + (size_t)(m0_ + 64 * wave + prow) * K + pch * 8;
-    fw_p = W + (size_t)(n0_ + 64 * wave + prow) * K + pch * 8;
-  };
-  auto advance = [&]() {
-    if (f_kt + 1 < nk) {
-      ++f_kt;
-      fa_p += 64;
-      fw_p += 64;
-    } else if (f_ti + 1 < ntiles) {
-      ++f_ti;
-      f_kt = 0;
-      cursor_tile(f_ti);
-    }   // past the last K-tile: stay (re-fetch into stages nobody reads again)
-  };
-  bool fetch_on = true;   // DIAG 1: off after the prologue
-  auto fetch = [&](int q, int st) {   // piece q (0-7 A, 8-15 W) into stage st
-    if constexpr (DIAG == 1) {
-      if (!fetch_on) return;
-    }
-    const char* dst = smem + st * STAGE + (q < 8 ? 0 : WOFF) + (8 * wave + (q & 7)) * 1024;
-    glds16_hidden((q < 8 ? fa_p : fw_p) + (q & 7) * pstride, dst);
-  };
-  // epilogue operands of tile ti into the parity area: bias (wave 0), column sums
-  // (wave 1), the 256 row statistics (waves 2-3, 2 rows per lane); a null bias is
-  // zero-filled. Full tiles only, so every row is in range.
-  auto ops_dma = [&](int ti) {
-    int m0_, n0_;
-    tile_of((int)blockIdx.x + ti * (int)gridDim.x, m0_, n0_);
-    char* o = smem + OPS + (ti & 1) * 4096;
-    int lo = lane;
-    asm volatile("" : "+v"(lo));
-    if (wave == 0) {
-      if (epi.bias)
-        glds16_hidden(epi.bias + n0_ + lo * 4, o);
-      else
-        ((float4*)o)[lane] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    if constexpr (LN) {
-      if (wave == 1) glds16_hidden(epi.colsum + n0_ + lo * 4, o + 1024);
-      if (wave >= 2)
-        glds16_hidden((const float*)(epi.stats + m0_ + (wave - 2) * 128 + 2 * lo),
-                      o + 2048 + (wave - 2) * 1024);
-    }
-  };
-
-  i16x8 fa[2][8], fb[2][8];
-
-  // epilogue of tile ti from the accumulators (see the header)
-  auto epilogue = [&](int ti) {
-    int m0, n0;
-    tile_of((int)blockIdx.x + ti * (int)gridDim.x, m0, n0);
-    const char* o = smem + OPS + (ti & 1) * 4096;
-    // the last MFMAs' results: 16 states before any accumulator read (asm MFMAs
-    // are opaque to hipcc's hazard recognizer)
-    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-    float4 tb[8], tc[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c4 = wc * 32 + 4 * j + fk;   // this lane's column quad of block j
-      tb[j] = ((const float4*)o)[c4];
-      tc[j] = LN ? ((const float4*)(o + 1024))[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    auto* outp = tr_out(epi);
-    const int ld = tr_ld(epi);
-    const int colb = n0 + wc * 128 + 16 * (fk & 1) + 8 * (fk >> 1);   // + 32p
-    static_for<8>([&](auto ic) {
-      constexpr int i = decltype(ic)::value;
-      const int rl = wr * 128 + 16 * i + fr;
-      auto* rowp = outp + (size_t)(m0 + rl) * ld + colb;
-      float2 st = make_float2(0.f, 0.f);
-      if constexpr (LN) st = ((const float2*)(o + 2048))[rl];
-      u32x4 xq[4];
-      if constexpr (RES) {
-#pragma unroll
-        for (int p = 0; p < 4; ++p) xq[p] = *(const u32x4*)(rowp + 32 * p);
-      }
-      static_for<4>([&](auto pc) {
-        constexpr int p = decltype(pc)::value;
-        const float4 v0 = acc_read<8 * i + 2 * p>(), v1 = acc_read<8 * i + 2 * p + 1>();
-        i16x4 o0, o1;
-        if constexpr (LN) {
-          o0 = epi.val4ln(v0, tb[2 * p], tc[2 * p], st);
-          o1 = epi.val4ln(v1, tb[2 * p + 1], tc[2 * p + 1], st);
-        } else {
-          o0 = epi.val4(v0, tb[2 * p]);
-          o1 = epi.val4(v1, tb[2 * p + 1]);
-        }
-        const u32x2 x0 = __builtin_bit_cast(u32x2, o0), x1 = __builtin_bit_cast(u32x2, o1);
-        // rows 1 / 3 of block 2p <-> rows 0 / 2 of block 2p+1: lane (fr, fk) then
-        // holds columns 8 (fk >> 1) .. +7 of block 2p + (fk & 1)
-        const auto s0 = __builtin_amdgcn_permlane16_swap(x0[0], x1[0], false, false);
-        const auto s1 = __builtin_amdgcn_permlane16_swap(x0[1], x1[1], false, false);
-        u32x4 w = {s0[0], s1[0], s0[1], s1[1]};
-        if constexpr (RES) {
-          unsigned t[4] = {w[0], w[1], w[2], w[3]};
-          const unsigned x[4] = {xq[p][0], xq[p][1], xq[p][2], xq[p][3]};
-          Epi::template add_x<4>(t, x);
-          w = (u32x4){t[0], t[1], t[2], t[3]};
-        }
-        if constexpr (DIAG == 2)
-          asm volatile("" ::"v"(w));
-        else
-          *(u32x4*)(rowp + 32 * p) = w;
-      });
-    });
-  };
-
-  if (ntiles > 0) {
-    // prologue: operands of tile 0, K-tiles 0 and 1 whole (K >= 128), then F(0)
-    cursor_tile(0);
-    ops_dma(0);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) fetch(q, 0);
-    advance();
-#pragma unroll
-    for (int q = 0; q < 16; ++q) fetch(q, 1);
-    advance();
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    lds_barrier();
-    fetch_on = DIAG != 1;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      fa[0][i] = *(const i16x8*)(smem + aoff0 + i * 2048);
-      fb[0][i] = *(const i16x8*)(smem + boff0 + i * 2048);
-    }
-
-    int G = 0;   // K-tiles this workgroup has entered (stage = G & 1)
-    for (int ti = 0; ti < ntiles; ++ti) {
-      for (int kt = 0; kt < nk; ++kt, ++G) {
-        const int st = G & 1;
-        // ---- even step 2G: multiply F(2G) (set 0), read F(2G+1) (stage st, half 1),
-        // DMA pieces DODD..15 of K-tile G+1 (G >= 1; K-tile 1 came whole in the prologue)
-        auto even = [&](auto first_c, auto dma_c) {
-          constexpr bool FIRST = decltype(first_c)::value, DMA = decltype(dma_c)::value;
-          const char* base = smem + st * STAGE;
-          static_for<8>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            fa[1][i] = *(const i16x8*)(base + aoff1 + i * 2048);
-            fb[1][i] = *(const i16x8*)(base + boff1 + i * 2048);
-            static_for<8>([&](auto jc) {
-              constexpr int j = decltype(jc)::value;
-              mfma_acc<T, 8 * i + j, FIRST>(fb[0][j], fa[0][i]);
-            });
-            if constexpr (DMA) {
-#pragma unroll
-              for (int q = lo(i, PE, EROWS); q < lo(i + 1, PE, EROWS); ++q) fetch(DODD + q, st ^ 1);
-            }
-          });
-          if constexpr (DMA) advance();
-        };
-        if (kt > 0)
-          even(std::false_type{}, std::true_type{});
-        else if (G > 0)
-          even(std::true_type{}, std::true_type{});
-        else
-          even(std::true_type{}, std::false_type{});
-
-        // ---- odd step 2G+1: K-tile G+1 has landed for every wave; stage st is free
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        lds_barrier();
-        if (kt == 0 && ti + 1 < ntiles) ops_dma(ti + 1);
-        {
-          const char* base = smem + (st ^ 1) * STAGE;
-          static_for<8>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            fa[0][i] = *(const i16x8*)(base + aoff0 + i * 2048);
-            fb[0][i] = *(const i16x8*)(base + boff0 + i * 2048);
-            static_for<8>([&](auto jc) {
-              constexpr int j = decltype(jc)::value;
-              mfma_acc<T, 8 * i + j, false>(fb[1][j], fa[1][i]);
-            });
-#pragma unroll
-            for (int q = lo(i, DODD, 8); q < lo(i + 1, DODD, 8); ++q) fetch(q, st);
-          });
-        }
-      }
-      // ---- this tile's epilogue; the next tile's K-tile 0 and F(0) are in flight
-      epilogue(ti);
-    }
-  }
-  // nothing may land in LDS unretired past this point
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // the row tail on the same workgroups
-  for (int task = blockIdx.x; task < ntail; task += gridDim.x) {
-    lds_barrier();
-    if (tail_wide)
-      gemm_tail_wg<T, Epi, 2, 128, 4>(A, W, M, N, K, epi, ntm_dp * 256, task, smem);
-    else
-      gemm_tail_wg<T, Epi, 1, 64, 4>(A, W, M, N, K, epi, ntm_dp * 256, task, smem);
-  }
-}
-
-#endif  // MICLIP_EXPERIMENTS
 
 // ---------------------------------------------------------------------------
 // Persistent form of the staggered 256x256 kernel (SCHED 2): one workgroup per
@@ -1994,594 +1638,6 @@ __global__ __launch_bounds__(512) void gemm256p_kernel(const T* __restrict__ A,
   }
   if (wr == 0) lds_barrier();   // balance the stagger barrier
 }
-#ifdef MICLIP_EXPERIMENTS
-// Experimental kernels (measured slower than the defaults): built
-// only into the diagnostic library (make exp -> build/exp/libmiclip_exp.so), never
-// into the product libmiclip.so.
-// ---------------------------------------------------------------------------
-// 256x256 tile, 256 threads = 4 waves (2x2), 128x128 per wave: ONE wave per
-// SIMD, its 8x8 grid of 16x16 fp32 fragments (256 registers) in the AGPR half
-// of the register file. Per 32-k step a wave reads 16 fragments (8 A + 8 B)
-// for 64 MFMAs -- half the LDS bytes per flop of the 8-wave 128x64 layout --
-// and it issues those reads for the NEXT step and its share of the LDS-DMA
-// between its own MFMAs, so the matrix pipe is fed without a partner wave.
-// LDS: 4 stages x 32 KiB (A 256 rows + W 256 rows of 64 B = 32 k each);
-// 16-B chunk c of row r at physical chunk c ^ (((r >> 2) & 1) << 1)
-// (conflict-free ds_read_b128 fragment reads; checked with the lane-group
-// bank model). Stage t+3 is DMA'd during step t and retired (own vmcnt +
-// the one barrier per step) at the top of step t+2: two steps of latency
-// slack. Register epilogue (quad transpose -> put4), one tile per workgroup.
-// Variant 300, not a default: parity-green, but same-process A/B on the
-// ViT-L/14 bs=256 shapes it is 15-40 % slower than the persistent 8-wave
-// kernel (c_proj 0.677 vs 0.479 ms): the 256 accumulators fill the AGPR half
-// exactly and hipcc bounces a few through VGPRs every step, and 64-B rows
-// halve the bytes per DMA row request. Kept as the starting point for a
-// one-wave-per-SIMD schedule.
-// ---------------------------------------------------------------------------
-template <typename T, class Epi>
-__global__ __launch_bounds__(256, 1) void gemm4w_kernel(const T* __restrict__ A,
-                                                        const T* __restrict__ W, int M, int N,
-                                                        int K, Epi epi, int gm) {
-  constexpr int STAGE = 32 * 1024, NS = 4;
-  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-  const int ntn = N / 256, ntm = (M + 255) / 256, nk = K / 32;
-  int tm, tn;
-  group_tile(xcd_remap(blockIdx.x, ntm * ntn), ntm, ntn, gm, tm, tn);
-  const int m0 = tm * 256, n0 = tn * 256;
-  // DMA pieces: 1 KiB = 16 rows x 64 B; stage piece p < 16: A rows 16p.., else
-  // W rows 16(p-16)..; wave w issues pieces 8w .. 8w+7 (waves 0-1 A, 2-3 W).
-  const int prow = lane >> 2;
-  const int lch = (lane & 3) ^ (((prow >> 2) & 1) << 1);
-  // one base pointer per lane + 32-bit row offsets (A rows clamped to M-1:
-  // finite duplicates of the last row, never stored)
-  const T* base = wave < 2 ? A + lch * 8 : W + (size_t)n0 * K + lch * 8;
-  unsigned roff[8];
-#pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    const int piece = (wave & 1) * 8 + p;
-    int r = piece * 16 + prow;
-    if (wave < 2) r = m0 + r < M ? m0 + r : M - 1;
-    roff[p] = (unsigned)r * (unsigned)K;
-  }
-  // stages past the last one re-fetch the last stage into a dead buffer, so
-  // every step issues exactly 8 DMAs per wave (branch-free, fixed vmcnt)
-  auto dma = [&](int kt, int p) {
-    kt = kt < nk ? kt : nk - 1;
-    glds16_hidden(base + roff[p] + kt * 32,
-                  smem + (kt & (NS - 1)) * STAGE + (wave * 8 + p) * 1024);
-  };
-  const int fr = lane & 15, fk = lane >> 4;
-  const int sw = (fk ^ (((fr >> 2) & 1) << 1)) << 4;
-  const int aoff = (wr * 128 + fr) * 64 + sw;
-  const int boff = 16384 + (wc * 128 + fr) * 64 + sw;
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // A fragments single-buffered (fa[g] is reloaded for the next step right
-  // after group g's MFMAs, its last use), W fragments double-buffered (every
-  // group reads all 8): 96 fragment VGPRs next to the 256 AGPR accumulators
-  i16x8 fa[8], fb[2][8];
-
-  // prologue: stages 0..2 in flight, stage 0 retired, F(0) read
-#pragma unroll
-  for (int s = 0; s < 3; ++s)
-#pragma unroll
-    for (int p = 0; p < 8; ++p) dma(s, p);
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  lds_barrier();
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    fa[i] = *(const i16x8*)(smem + aoff + i * 1024);
-    fb[0][i] = *(const i16x8*)(smem + boff + i * 1024);
-  }
-
-  auto step = [&](int t, auto par) {
-    constexpr int cur = decltype(par)::value, nxt = cur ^ 1;
-    // retire this wave's DMA of stage t+1 (8 younger: stage t+2's); the
-    // barrier makes every wave's visible and ends all reads of stage t-1's
-    // buffer (= stage t+3's). Past the last stage the reads and DMAs are
-    // harmless duplicates (dead buffers), so the step stays branch-free.
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    lds_barrier();
-    const char* nb = smem + ((t + 1) & (NS - 1)) * STAGE;
-#pragma unroll
-    for (int g = 0; g < 8; ++g) {
-      dma(t + 3, g);
-      fb[nxt][g] = *(const i16x8*)(nb + boff + g * 1024);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[g][j] = Mfma<T>::m16(fa[g], fb[cur][j], acc[g][j]);
-      __builtin_amdgcn_s_setprio(0);
-      fa[g] = *(const i16x8*)(nb + aoff + g * 1024);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  // K % 64 == 0 (launch check): steps come in pairs, one per register set
-  for (int t = 0; t < nk; t += 2) {
-    step(t, std::integral_constant<int, 0>{});
-    step(t + 1, std::integral_constant<int, 1>{});
-  }
-  // no LDS-DMA may land after the workgroup's LDS is handed to the next one
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  // epilogue straight from the accumulators
-  const int q = (lane & 15) >> 2, jj = lane & 3;
-  float4 bv[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) bv[j] = epi.bias4nb(n0 + wc * 128 + j * 16 + 4 * q);
-  const bool full = m0 + 256 <= M;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int row = m0 + wr * 128 + i * 16 + fk * 4 + jj;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int col = n0 + wc * 128 + j * 16 + 4 * q;
-      const float4 v = quad_transpose(acc[i][j], lane);
-      if (full || row < M) epi.put4(row, col, v, bv[j]);
-    }
-  }
-}
-// ---------------------------------------------------------------------------
-// 256x128x32 tile, 256 threads = 4 waves as 2(M) x 2(N), 128x64 per wave,
-// three LDS stages of 24 KiB (72 KiB per workgroup) so TWO workgroups share a
-// CU: one workgroup's prologue/epilogue (HBM-burst bound) overlaps the other's
-// MFMA main loop instead of idling the matrix pipes. 64-B LDS rows, 16-B
-// chunks swizzled by (row>>1)&3 (conflict-free 16x16x32 fragment reads under
-// the gfx950 ds_read_b128 lane groups). Prefetch distance two K-steps:
-// vmcnt(6) once per K-step (6 LDS-DMA per lane per stage).
-// ---------------------------------------------------------------------------
-template <typename T, class Epi>
-__global__ __launch_bounds__(256, 2) void gemm_t2_kernel(const T* __restrict__ A,
-                                                         const T* __restrict__ W, int M, int N,
-                                                         int K, Epi epi) {
-  constexpr int BM = 256, BN = 128, BKk = 32;
-  constexpr int A_BYTES = BM * 64, STAGE = (BM + BN) * 64;   // 16 KiB + 8 KiB
-  constexpr int EPI_LD = 132;
-  constexpr int SMEM = 3 * STAGE > 128 * EPI_LD * 4 ? 3 * STAGE : 128 * EPI_LD * 4;
-  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-  const int ntn = N / BN, ntm = (M + BM - 1) / BM;
-  const int bid = xcd_remap(blockIdx.x, ntm * ntn);
-  const int tm = bid / ntn, tn = bid - tm * ntn;
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  // LDS-DMA: piece = 16 rows x 64 B; lane -> row lane>>2, physical chunk lane&3
-  const int lchunk = (lane & 3) ^ ((lane >> 3) & 3);
-  const T* asrc[4];
-  const T* bsrc[2];
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    int r = m0 + (wave * 4 + p) * 16 + (lane >> 2);
-    r = r < M ? r : M - 1;
-    asrc[p] = A + (size_t)r * K + lchunk * 8;
-  }
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int c = n0 + (wave * 2 + p) * 16 + (lane >> 2);
-    bsrc[p] = W + (size_t)c * K + lchunk * 8;
-  }
-  auto stage = [&](int buf, int k0) {
-    char* sa = smem + buf * STAGE;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) glds16(asrc[p] + k0, sa + (wave * 4 + p) * 1024);
-#pragma unroll
-    for (int p = 0; p < 2; ++p) glds16(bsrc[p] + k0, sa + A_BYTES + (wave * 2 + p) * 1024);
-  };
-
-  const int fr = lane & 15, fk = lane >> 4;
-  const int swz = (fk ^ ((fr >> 1) & 3)) << 4;
-  const int aoff = (wr * 128 + fr) * 64 + swz;
-  const int boff = A_BYTES + (wc * 64 + fr) * 64 + swz;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = K / BKk;
-  stage(0, 0);
-  if (nk > 1) stage(1, BKk);
-  int cur = 0;
-  for (int t = 0; t < nk; ++t) {
-    if (t + 1 < nk)
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
-    if (t + 2 < nk) stage(cur == 0 ? 2 : cur - 1, (t + 2) * BKk);
-    const char* sb = smem + cur * STAGE;
-    i16x8 af[8], bf[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bf[j] = *(const i16x8*)(sb + boff + j * 1024);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) af[i] = *(const i16x8*)(sb + aoff + i * 1024);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = Mfma<T>::m16(af[i], bf[j], acc[i][j]);
-    __builtin_amdgcn_s_setprio(0);
-    cur = cur == 2 ? 0 : cur + 1;
-  }
-
-  // epilogue: two passes (wr), 128 rows x 128 cols fp32 staged, 512-B row reads
-  float* stg = (float*)smem;
-  const int ec = (tid & 31) * 4;
-  const float4 bv = epi.bias4(n0 + ec);
-  const bool full = m0 + BM <= M;
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    lds_barrier();
-    if (wr == q) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            stg[(i * 16 + fk * 4 + r) * EPI_LD + wc * 64 + j * 16 + fr] = acc[i][j][r];
-    }
-    lds_barrier();
-#pragma unroll 4
-    for (int k = 0; k < 16; ++k) {
-      const int lr = (tid >> 5) + 8 * k;
-      const int row = m0 + q * 128 + lr;
-      const float4 v = *(const float4*)(stg + lr * EPI_LD + ec);
-      if (full || row < M) epi.put4(row, n0 + ec, v, bv);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Ping-pong persistent GEMM (variant 400): TWO workgroups per CU, each 4 waves
-// (one per SIMD) walking 256x128 tiles with its own LDS ring, so one
-// workgroup's epilogue (VALU-bound: folded LN, QuickGELU, conversion; or the
-// residual read-modify-write) runs beside the other workgroup's MFMA main loop
-// on every SIMD instead of idling the matrix pipes (the 8-wave 256x256 kernel
-// spends ~23 % of a c_fc launch in its epilogue with the pipes idle).
-//   * per wave 128x64 outputs (8x4 16x16 fp32 fragments, 128 registers), the
-//     MFMA operands swapped for TrAcc epilogues (lane = row fr, 4 consecutive
-//     columns) exactly as the 8-wave kernel, same v_mfma_f32_16x16x32 chain in
-//     the same k order (32-k steps ascending), so tiles, tails and the other
-//     kernels stay bit-identical (batch invariance);
-//   * K in 32-k steps through a 3-slot ring (A 256 x 64 B + W 128 x 64 B =
-//     24 KiB per slot), LDS-DMA 2 steps ahead; fragments for step g+1 are read
-//     (into the other register set) before step g's MFMAs, so the only waits are
-//     one counted vmcnt + one 4-wave barrier per step. The ring runs on across
-//     tiles: the next tile's first steps are in flight (and its first
-//     fragments in registers) while this tile's epilogue runs;
-//   * 64-B LDS rows, 16-B chunk c of row r at c ^ ((r >> 1) & 3): conflict-free
-//     ds_read_b128 fragment reads under gfx950's lane groups;
-//   * register epilogue: one v_permlane16_swap per dword turns two row blocks'
-//     8-B column quads into 16-B row pieces (8 columns of one row per lane),
-//     stored straight from registers: no LDS staging, so the ring never stops;
-//   * the second workgroup on each CU starts `delay` 100-MHz ticks late so the
-//     two run half an epilogue out of phase (in phase, their epilogues would
-//     coincide and nothing would overlap).
-// The last tile-row may be partial (rows clamped on load, guarded on store).
-// ---------------------------------------------------------------------------
-// 16-byte LDS-DMA through a buffer descriptor (buffer_load_dwordx4 ... lds): byte
-// offset = lane part `vlane` (a VGPR) + wave-uniform part `soff` (an SGPR), added
-// INSIDE the statement so hipcc cannot strength-reduce the offsets into one
-// live VGPR per DMA (its loop-carried copies spilled, and the reloads put
-// vmcnt(0) waits into the K loop); `lds` an LDS byte address (wave-uniform).
-// The whole offset is range-checked: lanes past the descriptor's byte count
-// fetch nothing (rows past M of a partial tile: never stored).
-MICLIP_DEV void bdma16(unsigned vlane, unsigned soff, __amdgpu_buffer_rsrc_t rsrc, unsigned lds) {
-  unsigned keep, tmp;
-  asm volatile(
-      "v_add_u32 %1, %3, %2\n\t"
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %5\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %4, 0 offen lds\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep), "=&v"(tmp)
-      : "v"(vlane), "s"(soff), "s"(rsrc), "s"(lds)
-      : "memory");
-}
-
-// s_waitcnt vmcnt(n), n wave-uniform in [0, 63]
-MICLIP_DEV void wait_vmcnt63(int n) {
-  switch (n) {
-#define MICLIP_VMC(k) \
-  case k:           \
-    asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-    MICLIP_VMC(0) MICLIP_VMC(1) MICLIP_VMC(2) MICLIP_VMC(3) MICLIP_VMC(4) MICLIP_VMC(5)
-    MICLIP_VMC(6) MICLIP_VMC(7) MICLIP_VMC(8) MICLIP_VMC(9) MICLIP_VMC(10) MICLIP_VMC(11)
-    MICLIP_VMC(12) MICLIP_VMC(13) MICLIP_VMC(14) MICLIP_VMC(15) MICLIP_VMC(16) MICLIP_VMC(17)
-    MICLIP_VMC(18) MICLIP_VMC(19) MICLIP_VMC(20) MICLIP_VMC(21) MICLIP_VMC(22) MICLIP_VMC(23)
-    MICLIP_VMC(24) MICLIP_VMC(25) MICLIP_VMC(26) MICLIP_VMC(27) MICLIP_VMC(28) MICLIP_VMC(29)
-    MICLIP_VMC(30) MICLIP_VMC(31) MICLIP_VMC(32) MICLIP_VMC(33) MICLIP_VMC(34) MICLIP_VMC(35)
-    MICLIP_VMC(36) MICLIP_VMC(37) MICLIP_VMC(38) MICLIP_VMC(39) MICLIP_VMC(40) MICLIP_VMC(41)
-    MICLIP_VMC(42) MICLIP_VMC(43) MICLIP_VMC(44) MICLIP_VMC(45) MICLIP_VMC(46) MICLIP_VMC(47)
-#undef MICLIP_VMC
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-
-// epilogue global operations per lane of a full tile (stores, + residual loads)
-template <class Epi> struct PPEpiOps { static constexpr int n = 16; };
-template <> struct PPEpiOps<EpiResidual<_Float16>> { static constexpr int n = 32; };
-
-// 4-byte LDS-DMA of one dword into a dead LDS word: pads a wave's VM counter so
-// every wave's counted waits use the same compile-time counts
-MICLIP_DEV void vm_pad(const void* g, const void* lds) { glds4_hidden(g, lds); }
-
-template <typename T, class Epi>
-__global__ __launch_bounds__(256, 2) void gemm_pp_kernel(const T* __restrict__ A,
-                                                         const T* __restrict__ W, int M, int N,
-                                                         int K, Epi epi, int gm, int ntm,
-                                                         int delay) {
-  static_assert(TrAcc<Epi>::value, "gemm_pp_kernel: transposed-accumulator epilogues only");
-  constexpr int NS = 3, A_BYTES = 256 * 64, STAGE = A_BYTES + 128 * 64;   // 16 + 8 KiB
-  constexpr int OPS = NS * STAGE;
-  constexpr bool LN = IsLN<Epi>::value;
-  constexpr bool RES = PrefetchX<Epi>::value;
-  // VM-counter bookkeeping (per lane, per wave): D = LDS-DMA per step, C = the
-  // operand DMAs at a tile's first step (bias / column sums by wave 0, the row
-  // statistics by every wave, padded to the same count on every wave), E = the
-  // epilogue's global ops (stores, + residual loads)
-  constexpr int D = 6, C = LN ? 3 : 1, E = PPEpiOps<Epi>::n;
-  __shared__ __attribute__((aligned(1024))) char smem[OPS + 4096];
-  float4* tbias = (float4*)(smem + OPS);            // [32] bias column quads
-  float4* tcs = (float4*)(smem + OPS + 512);        // [32] column-sum quads (LN)
-  float2* tst = (float2*)(smem + OPS + 1024);       // [256] {mean, rstd} (LN)
-  char* sink = smem + OPS + 3072;                   // vm_pad destination (never read)
-
-  const int ntn = N / 128, ntiles = ntm * ntn, nk = K / 32;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-  const int fr = lane & 15, fk = lane >> 4;
-  const int swz = (fk ^ ((fr >> 1) & 3)) << 4;
-  const int aoff = (wr * 128 + fr) * 64 + swz;
-  const int boff = A_BYTES + (wc * 64 + fr) * 64 + swz;
-  const int prow = lane >> 2, lch = (lane & 3) ^ ((lane >> 3) & 3);
-
-  if (delay > 0 && (int)blockIdx.x >= (int)(gridDim.x >> 1)) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)delay)
-      __builtin_amdgcn_s_sleep(8);
-  }
-
-  // LDS-DMA through buffer descriptors: per lane one VGPR (its row and 16-B
-  // chunk within a 16-row piece), the rest wave-uniform; A rows past M fall
-  // outside A's descriptor (partial last tile-row)
-  const unsigned lbase = (unsigned)prow * (unsigned)K * 2u + (unsigned)lch * 16u;
-  const __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)A, (short)0, (int)((unsigned)M * (unsigned)K * 2u), 0x00020000);
-  const __amdgpu_buffer_rsrc_t wrsrc = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)W, (short)0, (int)((unsigned)N * (unsigned)K * 2u), 0x00020000);
-  const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(LDS_AS char*)smem);
-  unsigned arow0 = 0, brow0 = 0;   // byte offsets of the fetched tile's first A / W row
-  auto set_sources = [&](int m0_, int n0_) {
-    arow0 = (unsigned)(m0_ + wave * 64) * (unsigned)K * 2u;
-    brow0 = (unsigned)(n0_ + wave * 32) * (unsigned)K * 2u;
-  };
-  const unsigned piece_bytes = 16u * (unsigned)K * 2u;
-  auto dma_step = [&](int t, int slot_) {
-    const unsigned st = lds0 + slot_ * STAGE;
-    const unsigned kb = (unsigned)t * 64u;
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-      bdma16(lbase, __builtin_amdgcn_readfirstlane(arow0 + p * piece_bytes + kb), arsrc,
-             st + (wave * 4 + p) * 1024);
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-      bdma16(lbase, __builtin_amdgcn_readfirstlane(brow0 + p * piece_bytes + kb), wrsrc,
-             st + A_BYTES + (wave * 2 + p) * 1024);
-  };
-  auto tile_of = [&](int id, int& m0_, int& n0_) {
-    int tm, tn;
-    group_tile(xcd_remap(id, ntiles), ntm, ntn, gm, tm, tn);
-    m0_ = tm * 256;
-    n0_ = tn * 128;
-  };
-  // the tile's epilogue operands into LDS (retired by the step waits, published by
-  // the step barriers long before the epilogue reads them): exactly C per wave
-  auto dma_operands = [&](int m0_, int n0_) {
-    int lo = lane;
-    asm volatile("" : "+v"(lo));
-    if (wave == 0) {
-      const float* src = epi.bias + n0_ + (lo & 31) * 4;
-      if constexpr (LN) {
-        if (lo >= 32) src = epi.colsum + n0_ + (lo & 31) * 4;
-      }
-      glds16_hidden(src, tbias);
-    } else {
-      vm_pad(epi.bias, sink);
-    }
-    if constexpr (LN) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int d = wave * 128 + h * 64 + lo, r = m0_ + (d >> 1);
-        glds4_hidden((const float*)(epi.stats + (r < M ? r : M - 1)) + (d & 1),
-                     (const char*)tst + wave * 512 + h * 256);
-      }
-    }
-  };
-
-  f32x4 acc[8][4];
-  // A fragments single-buffered (fa[i] is reloaded for the next step right after
-  // its last MFMA of this step), W fragments double-buffered (every A fragment
-  // meets all four): 64 fragment VGPRs beside the 128 accumulators
-  i16x8 fa[8], fb[2][4];
-  auto read_a = [&](int slot_, int i) {
-    fa[i] = *(const i16x8*)(smem + slot_ * STAGE + aoff + i * 1024);
-  };
-  auto read_b = [&](int slot_, auto par_c) {
-    constexpr int P = decltype(par_c)::value;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) fb[P][j] = *(const i16x8*)(smem + slot_ * STAGE + boff + j * 1024);
-  };
-  // step's MFMAs (W fragments of set P); nslot >= 0: read the next step's A
-  // fragments from that slot as this step's uses of them end
-  auto mfmas = [&](auto par_c, auto first_c, int nslot) {
-    constexpr int P = decltype(par_c)::value;
-    constexpr bool FIRST = decltype(first_c)::value;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const f32x4 c = FIRST ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[i][j];
-        acc[i][j] = Mfma<T>::m16(fb[P][j], fa[i], c);   // C^T = W . A^T
-      }
-      if (nslot >= 0) read_a(nslot, i);
-    }
-  };
-
-  int id = blockIdx.x;
-  if (id >= ntiles) return;
-  int m0, n0;
-  tile_of(id, m0, n0);
-  set_sources(m0, n0);
-  // prologue: steps 0..2 in flight, E pad DMAs standing in for a previous tile's
-  // epilogue ops (so the first tile's counted waits are the steady-state ones),
-  // step 0 landed and its fragments read
-  int slot = 0;                  // slot of the current step
-  dma_step(0, 0);
-  dma_step(1, 1);
-  dma_step(2, 2);
-#pragma unroll
-  for (int e = 0; e < E; ++e) vm_pad(epi.bias, sink);
-  wait_vmcnt63(2 * D + E);
-  lds_barrier();
-  read_b(0, std::integral_constant<int, 0>{});
-#pragma unroll
-  for (int i = 0; i < 8; ++i) read_a(0, i);
-  __builtin_amdgcn_s_setprio(1);
-  for (;;) {
-    const int nid = id + gridDim.x;
-    const bool has_next = nid < ntiles;
-    int nm0 = 0, nn0 = 0;
-    if (has_next) tile_of(nid, nm0, nn0);
-    const bool full = m0 + 256 <= M;
-    // one 32-k step: t = local step, P = register set holding step t's fragments.
-    // Ops issued after step t+1's DMA (at step t-2) in the steady stream: the DMA
-    // of step t+2, and for t <= 2 the epilogue ops between the tiles (t = 0, 1)
-    // and the operand DMAs of this tile's first step (t = 1, 2). One body for
-    // every t (a peeled copy per t made hipcc rename, copy and spill
-    // accumulators), the count picked by a wave-uniform branch.
-    auto step = [&](int t, auto par_c) {
-      constexpr int P = decltype(par_c)::value;
-      const bool tail = !has_next && t + 2 >= nk;   // the stream's last two steps
-      if (!tail) {
-        switch (t < 3 ? t : 3) {
-          case 0: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D + E) : "memory"); break;
-          case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D + E + C) : "memory"); break;
-          case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D + C) : "memory"); break;
-          default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D) : "memory"); break;
-        }
-      } else if (t + 2 == nk) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no step t+2 exists
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      lds_barrier();
-      // refill the slot step t's fragments were read from (every wave is past
-      // this barrier, its reads retired by the lgkmcnt above)
-      if (t + 3 < nk) {
-        dma_step(t + 3, slot);
-      } else if (has_next) {
-        if (t + 3 == nk) set_sources(nm0, nn0);
-        dma_step(t + 3 - nk, slot);
-      }
-      if (t == 0) dma_operands(m0, n0);
-      const int nslot = slot == NS - 1 ? 0 : slot + 1;
-      // the next tile's first fragments are read after the epilogue (not live
-      // across it: the epilogue needs the registers)
-      const bool more1 = t + 1 < nk;
-      if (more1) read_b(nslot, std::integral_constant<int, P ^ 1>{});
-      mfmas(par_c, std::false_type{}, more1 ? nslot : -1);
-      slot = nslot;
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int t = 0; t < nk; t += 2) {
-      step(t, I0{});
-      step(t + 1, I1{});
-    }
-
-    // ---- epilogue from registers (TR: lane = row fr, columns 4fk .. 4fk+3) ----
-    __builtin_amdgcn_s_setprio(0);
-    auto* cb = tr_out(epi);
-    const int ld = tr_ld(epi);
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      // rows of blocks 2p (lanes fk even) and 2p+1 (fk odd) after the swap
-      const int row = m0 + wr * 128 + (2 * p + (fk & 1)) * 16 + fr;
-      const int rowc = row < M ? row : M - 1;
-      const int col = n0 + wc * 64 + (fk >> 1) * 8;
-      u32x4 xq[4];
-      if constexpr (RES) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) xq[j] = *(const u32x4*)(cb + (size_t)rowc * ld + col + j * 16);
-      }
-      float2 s0 = make_float2(0.f, 0.f), s1 = make_float2(0.f, 0.f);
-      if constexpr (LN) {
-        s0 = tst[wr * 128 + (2 * p) * 16 + fr];
-        s1 = tst[wr * 128 + (2 * p + 1) * 16 + fr];
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float4 bq = tbias[wc * 16 + j * 4 + fk];
-        const f32x4 a0 = acc[2 * p][j], a1 = acc[2 * p + 1][j];
-        const float4 v0 = make_float4(a0[0], a0[1], a0[2], a0[3]);
-        const float4 v1 = make_float4(a1[0], a1[1], a1[2], a1[3]);
-        i16x4 o0, o1;
-        if constexpr (LN) {
-          const float4 cq = tcs[wc * 16 + j * 4 + fk];
-          o0 = epi.val4ln(v0, bq, cq, s0);
-          o1 = epi.val4ln(v1, bq, cq, s1);
-        } else {
-          o0 = epi.val4(v0, bq);
-          o1 = epi.val4(v1, bq);
-        }
-        const u32x2 u = __builtin_bit_cast(u32x2, o0), v = __builtin_bit_cast(u32x2, o1);
-        // 16-lane rows: the fk-odd rows of u <-> the fk-even rows of v
-        const auto w0 = __builtin_amdgcn_permlane16_swap(u[0], v[0], false, false);
-        const auto w1 = __builtin_amdgcn_permlane16_swap(u[1], v[1], false, false);
-        u32x4 w = {w0[0], w1[0], w0[1], w1[1]};
-        if constexpr (RES) {
-          unsigned tt[4] = {w[0], w[1], w[2], w[3]};
-          const unsigned xx[4] = {xq[j][0], xq[j][1], xq[j][2], xq[j][3]};
-          Epi::template add_x<4>(tt, xx);
-          w = (u32x4){tt[0], tt[1], tt[2], tt[3]};
-        }
-        if (full || row < M) *(u32x4*)(cb + (size_t)row * ld + col + j * 16) = w;
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    __builtin_amdgcn_s_setprio(1);
-    if (!has_next) break;
-    // the next tile's step-0 fragments (its DMA was retired and published at
-    // this tile's last step)
-    read_b(slot, std::integral_constant<int, 0>{});
-#pragma unroll
-    for (int i = 0; i < 8; ++i) read_a(slot, i);
-    // a partial tile issued fewer than E ops: drain, so the next tile's counted
-    // waits (which assume E younger ops) can only over-wait
-    if (!full) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    id = nid;
-    m0 = nm0;
-    n0 = nn0;
-  }
-  // nothing may land in LDS after the workgroup retires
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-#endif  // MICLIP_EXPERIMENTS
 
 // Kernel variants and schedule switches are chosen by the op-level `variant`
 // argument only (miclip_op_gemm: A/B benches); the model path runs variant 0,
@@ -2678,111 +1734,7 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   variant %= 1000;
   const bool env_variant = false;   // an explicit variant never falls back silently
   if (variant != 0 && variant != 128 && variant != 256 && variant != 257 && variant != 258 &&
-      variant != 259 && variant != 260 && variant != 2 && variant != 3 && variant != 300 &&
-      variant != 192 &&
-      !(variant >= 400 && variant < 420) && variant != 508 && variant != 516 &&
-      !(variant >= 530 && variant <= 534))
-    return hipErrorInvalidValue;
-#ifdef MICLIP_EXPERIMENTS
-  if constexpr (TrAcc<Epi>::value && !std::is_same_v<Epi, EpiResidual<float>>) {
-    // ping-pong kernel: variant 400 + d = start delay of the second workgroup per
-    // CU in microseconds
-    if (variant >= 400 && variant < 420) {
-      if (N % 128 || K % 64 || K < 128 || !epi.bias) {
-        if (!env_variant) return hipErrorInvalidValue;
-        variant = 0;
-      }
-    }
-    if (variant >= 400 && variant < 420) {
-      const int ntm = (M + 255) / 256, ntiles = ntm * (N / 128), ncu = cu_count();
-      const int grid = ntiles < 2 * ncu ? ntiles : 2 * ncu;
-      hipLaunchKernelGGL((gemm_pp_kernel<T, Epi>), dim3(grid), dim3(256), 0, s, (const T*)A,
-                         (const T*)W, M, N, K, epi, gm, ntm, (variant - 400) * 100);
-      return hipGetLastError();
-    }
-  }
-  if (variant >= 400 && variant < 420) {
-    if (!env_variant) return hipErrorInvalidValue;
-    variant = 0;
-  }
-  if constexpr (!IsPatch<Epi>::value) {
-    if (variant == 300 && N % 256 == 0 && K % 64 == 0) {
-      // 4-wave 128x128-per-wave kernel (A/B prototype), one tile per workgroup
-      const int tiles = ((M + 255) / 256) * (N / 256);
-      hipLaunchKernelGGL((gemm4w_kernel<T, Epi>), dim3(tiles), dim3(256), 0, s, (const T*)A,
-                         (const T*)W, M, N, K, epi, gm);
-      return hipGetLastError();
-    }
-  }
-  if constexpr (TrAcc<Epi>::value && !IsPatch<Epi>::value &&
-                !std::is_same_v<Epi, EpiResidual<float>>) {
-    // 4-wave persistent kernel (gemm4s_kernel): variant 500 + DODD (DMA pieces of
-    // a K-tile issued in the odd k-step; the rest in the even one)
-    if (variant == 508 || variant == 516 || (variant >= 530 && variant <= 534)) {
-      if (N % 256 || K % 64 || K < 128 || M < 256) return hipErrorInvalidValue;
-      // full 256-row tiles only: plan_tail's whole rounds when it splits, else every
-      // full tile-row, the rest (< 256 rows, or <= 256 after whole rounds) as tail tasks
-      TailPlan tp = plan_tail(M, N);
-      if (tp.ntm_dp * 256 > M || notail) {
-        tp.ntm_dp = M / 256;
-        const int rows = M - tp.ntm_dp * 256;
-        tp.wgs = rows > 0 ? (rows + 15) / 16 * (N / 64) : 0;
-        tp.wide = 0;
-      }
-      const int ndp = tp.ntm_dp * (N / 256), ncu = cu_count();
-      const int grid = ndp < ncu ? (ndp > 0 ? ndp : 1) : ncu;
-      if constexpr (std::is_same_v<Epi, EpiResidual<_Float16>> ||
-                    std::is_same_v<Epi, EpiStore<_Float16, ACT_QUICKGELU>>) {
-        if (diag == 1 && variant == 508) {
-          hipLaunchKernelGGL((gemm4s_kernel<T, Epi, 8, 1>), dim3(grid), dim3(256), 0, s,
-                             (const T*)A, (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs,
-                             tp.wide & 1);
-          return hipGetLastError();
-        }
-        if (diag == 2 && variant == 508) {
-          hipLaunchKernelGGL((gemm4s_kernel<T, Epi, 8, 2>), dim3(grid), dim3(256), 0, s,
-                             (const T*)A, (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs,
-                             tp.wide & 1);
-          return hipGetLastError();
-        }
-      }
-      if (diag) return hipErrorInvalidValue;
-      // DMA-spread experiments (fc / proj epilogues only): 530 (8, 8), 531 (8, 6),
-      // 532 (10, 6), 533 (12, 4), 534 (16, -): (DODD, EROWS)
-      if constexpr (std::is_same_v<Epi, EpiResidual<_Float16>> ||
-                    std::is_same_v<Epi, EpiStore<_Float16, ACT_QUICKGELU>>) {
-#define MICLIP_G4(V, D, E)                                                                 \
-  if (variant == V) {                                                                     \
-    hipLaunchKernelGGL((gemm4s_kernel<T, Epi, D, 0, E>), dim3(grid), dim3(256), 0, s,      \
-                       (const T*)A, (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs,     \
-                       tp.wide & 1);                                                      \
-    return hipGetLastError();                                                             \
-  }
-        MICLIP_G4(530, 8, 8) MICLIP_G4(531, 8, 6) MICLIP_G4(532, 10, 6) MICLIP_G4(533, 12, 4)
-        MICLIP_G4(534, 16, 1)
-#undef MICLIP_G4
-      }
-      if (variant >= 530) return hipErrorInvalidValue;
-      if (variant == 508)
-        hipLaunchKernelGGL((gemm4s_kernel<T, Epi, 8>), dim3(grid), dim3(256), 0, s, (const T*)A,
-                           (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs, tp.wide & 1);
-      else
-        hipLaunchKernelGGL((gemm4s_kernel<T, Epi, 16>), dim3(grid), dim3(256), 0, s,
-                           (const T*)A, (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs,
-                           tp.wide & 1);
-      return hipGetLastError();
-    }
-  }
-  if (variant == 2) {   // 256x128, two workgroups per CU
-    const int tiles = ((M + 255) / 256) * (N / 128);
-    hipLaunchKernelGGL((gemm_t2_kernel<T, Epi>), dim3(tiles), dim3(256), 0, s, (const T*)A,
-                       (const T*)W, M, N, K, epi);
-    return hipGetLastError();
-  }
-#endif  // MICLIP_EXPERIMENTS
-  // experimental variants: refused here (not applicable, or not in this build)
-  if ((variant >= 400 && variant < 420) || variant == 300 || variant == 2 || variant == 508 ||
-      variant == 516 || (variant >= 530 && variant <= 534))
+      variant != 259 && variant != 260 && variant != 3 && variant != 192)
     return hipErrorInvalidValue;
   // default for full-size problems: the persistent staggered kernel (variant
   // 259; same-process A/B vs 258 on the ViT-L/14 shapes: QKV +1 %, out-proj +9 %,

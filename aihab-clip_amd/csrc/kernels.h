@@ -125,7 +125,7 @@ hipError_t class_token(const float* cls, const float* pos, void* X, int B, int n
 hipError_t token_embed(const int64_t* tokens, const float* tok_emb, const float* pos, void* X,
                        int32_t* eot_rows, int P, int L, int D, int vocab, hipStream_t s,
                        int resid16 = 0);
-// out[r, :] = in[r, :] @ Wm  (fp32 on the f32 MFMA, Wm [D, E] row-major, D % 64 == 0)
+// out[r, :] = in[r, :] @ Wm  (fp32 on the f32 MFMA, Wm [D, E] row-major, D % 16 == 0)
 hipError_t rowvec_matmul(const float* in, const float* Wm, float* out, int R, int D, int E,
                          hipStream_t s);
 // fp32 [rows, src_cols] -> compute dtype [rows, cols] (cols >= src_cols, zero pad), RNE
@@ -134,7 +134,8 @@ hipError_t cast_pad(int dtype, const float* in, void* out, int64_t rows, int src
 // in-place row L2 normalisation (F.normalize, eps 1e-12), fp32 [R, D]
 hipError_t row_l2norm(float* x, int R, int D, hipStream_t s);
 // zero-shot head: f = normalize(x @ proj) (proj may be null -> f = normalize(x));
-// logits = scale * f @ tw ([E, C]); topk indices (sorted, largest first).
+// logits = scale * f @ tw ([E, C], E % 16 == 0) on the f32 MFMA with the row norm
+// fused (head_logits_kernel); topk indices (sorted, largest first; topk_rows_kernel).
 // With proj, scratch (fp32 [B, E]) receives the projection, which runs first as
 // a chip-wide f32-MFMA kernel (head_proj_kernel, also behind rowvec_matmul).
 hipError_t zero_shot(const float* x, const float* proj, const float* tw, float* logits,

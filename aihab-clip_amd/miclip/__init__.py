@@ -20,7 +20,13 @@ from .preprocess import Transform
 from .weights import generate_state_dict, synthetic_images
 
 __all__ = ["available_models", "load", "tokenize", "build_model", "CLIP", "CLIPConfig",
-           "MODEL_CONFIGS"]
+           "MODEL_CONFIGS", "SeededWeightsWarning"]
+
+
+class SeededWeightsWarning(UserWarning):
+    """A model name (or an open_clip pretrained tag) was resolved to seeded random
+    weights: no checkpoints exist offline. Filter it where that is intended
+    (benchmarks, tests); pass a state-dict path for real weights."""
 
 
 def _transform(n_px):
@@ -33,7 +39,8 @@ def load(name, device="cuda" if torch.cuda.is_available() else "cpu", jit=False,
     """Counterpart of clip.load (clip/clip.py:89-137): returns (state_dict, model, preprocess).
 
     `name` is a model name from available_models() -- resolved offline to the
-    CLIP shapes with seeded random weights (no checkpoints exist offline) -- or
+    CLIP shapes with seeded random weights (no checkpoints exist offline; a
+    SeededWeightsWarning says so, as for an open_clip pretrained tag) -- or
     a path to a state-dict checkpoint (loaded with weights_only=True). Anything
     else raises RuntimeError like the reference. `jit=True` is accepted with a
     warning and loads the non-JIT model (the reference does the same when the
@@ -53,6 +60,9 @@ def load(name, device="cuda" if torch.cuda.is_available() else "cpu", jit=False,
     if surface is None:
         surface = "open_clip" if name in OPEN_CLIP_MODELS else "openai"
     if name in MODEL_CONFIGS:
+        warnings.warn(f"{name}: no checkpoint offline; loading SEEDED RANDOM weights (seed={seed}). "
+                      f"Pass a state-dict file path for real weights.", SeededWeightsWarning,
+                      stacklevel=2)
         cfg = MODEL_CONFIGS[name]
         sd = generate_state_dict(cfg, seed=seed)
         sd = {k: torch.from_numpy(v) for k, v in sd.items()}

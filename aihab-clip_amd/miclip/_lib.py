@@ -9,12 +9,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MICLIP_LIB", os.path.join(_HERE, "libmiclip.so"))
-# the diagnostic library with the measured-slower experimental kernels (make exp);
-# tests of those kernels and A/B scripts load it explicitly
-EXP_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "build", "exp",
-                            "libmiclip_exp.so")
 
-ABI_VERSION = 8          # include/miclip.h MICLIP_ABI_VERSION
+ABI_VERSION = 9          # include/miclip.h MICLIP_ABI_VERSION
 MICLIP_FP16 = 0
 MICLIP_BF16 = 1
 MICLIP_MXFP8 = 2
@@ -31,6 +27,7 @@ MICLIP_MODEL_MXFP8 = 4
 MICLIP_MODEL_CLS_LAST = 8
 MICLIP_MODEL_MX_OUT = 16
 MICLIP_MODEL_MX_GELU_TANH = 32
+MICLIP_MODEL_LNFOLD_TEXT = 64
 # miclip_config.options (include/miclip.h MICLIP_OPT_*)
 MICLIP_OPT_RESID_F32 = 1
 MICLIP_OPT_NO_LN_FOLD = 2
@@ -45,7 +42,7 @@ EXPORTS = (
     "miclip_clock_probe",
     "miclip_model_destroy", "miclip_last_error", "miclip_abi_version",
     "miclip_model_bytes", "miclip_model_flags", "miclip_model_set_option", "miclip_set_gemm_variant", "miclip_set_profiling", "miclip_profile_read", "miclip_set_splits", "miclip_image_splits",
-    "miclip_op_gemm", "miclip_op_ln_stats", "miclip_op_ln_fold", "miclip_op_gemm_ln",
+    "miclip_op_gemm", "miclip_op_gemm_splitk", "miclip_op_ln_stats", "miclip_op_ln_fold", "miclip_op_gemm_ln",
     "miclip_op_layernorm", "miclip_op_attention", "miclip_op_attention_q0", "miclip_preprocess",
     "miclip_row_norms", "miclip_class_centroids", "miclip_proto_scores",
     "miclip_mx_scale_bytes", "miclip_op_quant_mx", "miclip_op_gemm_mx", "miclip_op_gemm_mx_v", "miclip_op_layernorm_mx",
@@ -122,6 +119,8 @@ def load_library(path: str = None):
         "miclip_op_attention_q0": ([i32, vp, vp, i32, i32, i32, i32, vp], ctypes.c_int),
         "miclip_op_ln_stats": ([vp, vp, i32, i32, vp, vp], ctypes.c_int),
         "miclip_op_ln_fold": ([i32, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, vp], ctypes.c_int),
+        "miclip_op_gemm_splitk": ([i32, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32,
+                                   vp, vp], ctypes.c_int),
         "miclip_op_gemm_ln": ([i32, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp],
                               ctypes.c_int),
         "miclip_op_attention": ([i32, vp, vp, i32, i32, i32, i32, i32, i32, vp], ctypes.c_int),
@@ -146,11 +145,6 @@ def load_library(path: str = None):
     if path is None:
         _lib = lib
     return lib
-
-
-def load_experiments():
-    """The experiments library (a separate handle; raises MiclipError if not built)."""
-    return load_library(EXP_LIB_PATH)
 
 
 def check(rc: int, what: str = ""):

@@ -145,6 +145,12 @@ class CLIP(nn.Module):
                  surface="openai", options=None):
         super().__init__()
         self._options = option_bits(options)
+        # runtime settings of the live handle (set_splits / set_gemm_variant /
+        # set_profiling; set_cls_last edits _options): re-applied to every new
+        # handle, so a device move keeps what the caller chose
+        self._splits = None
+        self._gemm_variants = {}
+        self._profiling = False
         if compute_dtype not in _DTYPES:
             raise ValueError(f"compute_dtype must be one of {sorted(_DTYPES)}")
         if surface not in SURFACES:
@@ -198,6 +204,12 @@ class CLIP(nn.Module):
         h = _Handle(self.config, _DTYPES[self.compute_dtype][0], idx, self._options)
         h.load_device(list(self.state_dict().items()))
         self._handle = h
+        if self._splits is not None:
+            self.set_splits(self._splits)
+        for which, variant in self._gemm_variants.items():
+            self.set_gemm_variant(which, variant)
+        if self._profiling:
+            self.set_profiling(True)
 
     def refresh_weights(self):
         """Re-upload Parameters after they were modified in place (device to device)."""
@@ -233,6 +245,7 @@ class CLIP(nn.Module):
         """Split encode_image batches over 2 HIP streams (default) or not (1)."""
         h = self._require()
         _lib.check(h.lib.miclip_set_splits(h.ptr, int(splits)), "miclip_set_splits")
+        self._splits = int(splits)
 
     def image_splits(self, batch):
         """Parts encode_image splits `batch` images into (miclip_image_splits)."""
@@ -247,7 +260,8 @@ class CLIP(nn.Module):
         h = self._require()
         f = h.lib.miclip_model_flags(h.ptr)
         return dict(resid16=bool(f & _lib.MICLIP_MODEL_RESID16),
-                    lnfold=bool(f & _lib.MICLIP_MODEL_LNFOLD),
+                    lnfold=bool(f & _lib.MICLIP_MODEL_LNFOLD),          # vision tower
+                    lnfold_text=bool(f & _lib.MICLIP_MODEL_LNFOLD_TEXT),
                     mxfp8=bool(f & _lib.MICLIP_MODEL_MXFP8),
                     cls_last=bool(f & _lib.MICLIP_MODEL_CLS_LAST),
                     mx_out=bool(f & _lib.MICLIP_MODEL_MX_OUT),
@@ -260,16 +274,20 @@ class CLIP(nn.Module):
         h = self._require()
         _lib.check(h.lib.miclip_set_gemm_variant(h.ptr, int(which), int(variant)),
                    "miclip_set_gemm_variant")
+        self._gemm_variants[int(which)] = int(variant)
 
     def set_cls_last(self, on=True):
         """Last vision block on the CLS rows only (default) or over every row."""
         h = self._require()
         _lib.check(h.lib.miclip_model_set_option(h.ptr, _lib.MICLIP_OPT_FULL_LAST_BLOCK,
                                                  int(not on)), "miclip_model_set_option")
+        bit = _lib.MICLIP_OPT_FULL_LAST_BLOCK
+        self._options = (self._options & ~bit) | (0 if on else bit)
 
     def set_profiling(self, enable=True):
         h = self._require()
         _lib.check(h.lib.miclip_set_profiling(h.ptr, int(bool(enable))), "miclip_set_profiling")
+        self._profiling = bool(enable)
 
     def profile_read(self, reset=True):
         """{kernel class: dict(launches, ms, flops, bytes)} from the HIP-event profiler."""

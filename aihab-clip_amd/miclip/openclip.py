@@ -14,8 +14,10 @@ open_clip's own code.
     `pretrained` = a state-dict file (built with the named model's config: exact
     GELU and 80-wide vision heads for ViT-H-14, shapes checked), or None /
     "seeded" for seeded weights of the named shape. A pretrained TAG (e.g.
-    "laion2b_s32b_b79k") raises: there are no checkpoints offline, and silently
-    returning random weights would make every downstream accuracy meaningless.
+    "openai", the reference config's default, or "laion2b_s32b_b79k") has no
+    checkpoint offline: it loads the seeded weights with a SeededWeightsWarning,
+    the same policy as `miclip.load(<model name>)`, so the reference's configs run
+    unchanged and random weights are never silent.
     Both transforms are the eval transform (Resize
     bicubic + CenterCrop + CLIP normalise, open_clip's default for the OpenAI
     mean/std): the training-time augmentation is outside the encode path.
@@ -28,6 +30,7 @@ lock_text_tower, backward through encode_image) is outside the encode path; the
 model's lock_* methods raise NotImplementedError saying so.
 """
 import os
+import warnings
 
 import torch
 
@@ -40,24 +43,28 @@ def list_models():
 
 def create_model(model_name, pretrained=None, device="cuda", *, compute_dtype="fp16", seed=0,
                  **_unused):
-    from . import load
+    from . import SeededWeightsWarning, load
     from .configs import MODEL_CONFIGS
     if model_name not in OPEN_CLIP_MODELS:
         raise RuntimeError(f"Model config for {model_name} not found; available models "
                            f"{list_models()}.")
-    if pretrained in (None, "", "seeded"):
-        src, config = model_name, None
-    elif os.path.isfile(str(pretrained)):
+    if pretrained not in (None, "", "seeded") and os.path.isfile(str(pretrained)):
         # the named model's architecture, not build_model's shape inference (which
         # would give QuickGELU and 64-wide heads); load() checks every shape
         src, config = str(pretrained), MODEL_CONFIGS[model_name]
     else:
-        raise RuntimeError(
-            f"pretrained={pretrained!r} for {model_name}: no pretrained checkpoints are "
-            f"available offline. Pass a state-dict file path, or pretrained=None / 'seeded' "
-            f"for seeded random weights of the {model_name} shapes.")
-    _, model, _ = load(src, device=device, compute_dtype=compute_dtype, seed=seed,
-                       surface="open_clip", config=config)
+        if pretrained not in (None, "", "seeded"):
+            warnings.warn(
+                f"pretrained={pretrained!r} for {model_name}: no pretrained checkpoints are "
+                f"available offline; loading SEEDED RANDOM weights (seed={seed}) of the "
+                f"{model_name} shapes. Pass a state-dict file path for real weights.",
+                SeededWeightsWarning, stacklevel=3)
+        src, config = model_name, None
+    with warnings.catch_warnings():
+        # the tag warning above (or the explicit None / "seeded") already said it
+        warnings.simplefilter("ignore", SeededWeightsWarning)
+        _, model, _ = load(src, device=device, compute_dtype=compute_dtype, seed=seed,
+                           surface="open_clip", config=config)
     return model
 
 

@@ -182,10 +182,14 @@ def attach_traffic(model_name, dtype, epi, M):
 # --------------------------------------------------------------------- rank --
 
 def _load_miclip(name, dev, dtype, options=None):
+    import warnings
     import miclip
-    # OpenAI surface for every model (pre-projection encode, projection in the head)
-    _, model, _ = miclip.load(name, device=dev, compute_dtype=dtype, surface="openai",
-                              options=options)
+    # OpenAI surface for every model (pre-projection encode, projection in the head);
+    # seeded random weights are the bench's stated synthetic data ("data" field)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", miclip.SeededWeightsWarning)
+        _, model, _ = miclip.load(name, device=dev, compute_dtype=dtype, surface="openai",
+                                  options=options)
     return model
 
 

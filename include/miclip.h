@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define MICLIP_ABI_VERSION 8
+#define MICLIP_ABI_VERSION 9
 
 enum miclip_status {
   MICLIP_OK = 0,
@@ -239,7 +239,9 @@ int miclip_abi_version(void);
 int64_t miclip_model_bytes(const miclip_model* m);
 /* Numerics path the handle runs (from miclip_config.options and the dtype):
  * MICLIP_MODEL_RESID16 fp16 residual stream, MICLIP_MODEL_LNFOLD ln_1 / ln_2 folded
- * into the QKV / c_fc GEMMs, MICLIP_MODEL_MXFP8 MX-fp8 GEMM operands (vision tower),
+ * into the vision tower's QKV / c_fc GEMMs (MICLIP_MODEL_LNFOLD_TEXT: the text
+ * tower's; MX-fp8 models fold the text tower only), MICLIP_MODEL_MXFP8 MX-fp8 GEMM
+ * operands (vision tower),
  * MICLIP_MODEL_CLS_LAST last vision block on the CLS rows, MICLIP_MODEL_MX_OUT MX-fp8
  * vision out-projection, MICLIP_MODEL_MX_GELU_TANH tanh-form GELU in the MX c_fc
  * epilogue. 0 for NULL. */
@@ -249,6 +251,7 @@ int64_t miclip_model_bytes(const miclip_model* m);
 #define MICLIP_MODEL_CLS_LAST 8
 #define MICLIP_MODEL_MX_OUT 16
 #define MICLIP_MODEL_MX_GELU_TANH 32
+#define MICLIP_MODEL_LNFOLD_TEXT 64
 int miclip_model_flags(const miclip_model* m);
 /* Diagnostics: the GEMM kernel of the block launches (>= 256 rows) --
  * which 0: the folded-LN store GEMMs (QKV, c_fc), 1: the fp16 residual GEMMs
@@ -306,6 +309,17 @@ int miclip_op_gemm(int32_t dtype, const void* A, const void* W, const float* bia
  *   x [R, D]; rscale = the fold's inv_scale (device), or NULL for 1.
  * miclip_op_gemm_ln: C [M, N] (dtype) = act(rs * (A . Wf^T - mean * colsum) + c), A [M, K]
  *   the un-normalised rows (act as miclip_op_gemm; variant as there). */
+/* The split-K GEMM of the CLS-only last vision block (gemm_nt_splitk_kernel +
+ * splitk_reduce_kernel), op level: sk K slices (K % (64 sk) == 0) summed in
+ * ascending order through ws (device fp32, >= sk * M * N floats), then the epilogue.
+ * epi 0: C dtype = act(. + bias); 1: C fp32 += . + bias; 4: C fp16 += . + bias (the
+ * fp16 residual stream); 5: the folded-LN store of miclip_op_gemm_ln (c, colsum,
+ * stats; act). N % 128 == 0. Replaces the CLS rows' Linear calls (clip/model.py:
+ * 171-175, 179-181 on ln_post's rows, :226-229). */
+int miclip_op_gemm_splitk(int32_t dtype, const void* A, const void* W, const float* bias,
+                          const float* c, const float* colsum, const float* stats, void* C,
+                          int32_t M, int32_t N, int32_t K, int32_t epi, int32_t act, int32_t sk,
+                          float* ws, void* stream);
 int miclip_op_ln_stats(const void* x, float* stats, int32_t R, int32_t D, const float* rscale,
                        void* stream);
 int miclip_op_ln_fold(int32_t dtype, const void* W, const float* gamma, const float* beta,

@@ -44,7 +44,7 @@ class StubModel:
         return 1
 
     def numerics(self):
-        return dict(resid16=True, lnfold=True, mxfp8=False, cls_last=True, mx_out=False,
+        return dict(resid16=True, lnfold=True, lnfold_text=True, mxfp8=False, cls_last=True, mx_out=False,
                     mx_gelu_tanh=False)
 
     def encode_text(self, toks):

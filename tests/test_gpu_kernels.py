@@ -21,16 +21,6 @@ def lib():
     return _lib.load_library()
 
 
-@pytest.fixture(scope="module")
-def exp_lib():
-    """The diagnostic library with the experimental kernels (make exp): variants
-    2 / 300 (GEMM) and 9 (attention) are not in the product libmiclip.so."""
-    if not torch.cuda.is_available():
-        pytest.skip("no HIP device")
-    from miclip import _lib
-    return _lib.load_experiments()
-
-
 def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
@@ -44,7 +34,6 @@ def _check(lib, rc):
                                           (1000, 768, 3072, 128), (1000, 768, 3072, 256),
                                           (300, 256, 192, 256), (257, 512, 64, 256),
                                           (4096, 1024, 1024, 0), (33, 2304, 768, 256),
-                                          (1000, 768, 3072, 2), (300, 256, 192, 2), (257, 512, 64, 2),
                                           (33, 2304, 768, 257), (600, 1024, 4096, 257),
                                           (1000, 768, 3072, 3), (300, 256, 192, 3), (257, 512, 64, 3),
                                           (65792, 1024, 128, 3), (2000, 2304, 256, 3),
@@ -55,16 +44,9 @@ def _check(lib, rc):
                                           (4096, 1024, 1024, 260), (33, 2304, 128, 260),
                                           (1000, 768, 3072, 259), (300, 256, 192, 259), (257, 512, 64, 259),
                                           (4096, 1024, 1024, 259), (33, 2304, 128, 259),
-                                          (65792, 1024, 1024, 259), (16448, 3072, 256, 259),
-                                          (1000, 768, 3072, 300), (300, 256, 192, 300), (257, 512, 64, 300),
-                                          (65792, 1024, 1024, 300), (16448, 3072, 256, 300)])
+                                          (65792, 1024, 1024, 259), (16448, 3072, 256, 259)])
 @pytest.mark.parametrize("epi,act", [(0, 0), (0, 1), (0, 2), (1, 0), (2, 0), (4, 0)])
-def test_gemm(lib, exp_lib, dt, M, N, K, variant, epi, act):
-    if variant in (2, 300):   # experimental kernels: refused by the product library
-        z = torch.zeros(M * max(N, K) + N * K, device="cuda")
-        assert lib.miclip_op_gemm(0, z.data_ptr(), z.data_ptr(), z.data_ptr(), z.data_ptr(), M, N, K,
-                                  epi, act, variant, _stream()) != 0
-        lib = exp_lib
+def test_gemm(lib, dt, M, N, K, variant, epi, act):
     code, tdt = DT[dt]
     g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K + epi * 3 + act)
     A = (torch.randn(M, K, device="cuda", generator=g) * 0.5).to(tdt)
@@ -337,46 +319,6 @@ def test_attention_x8_many_heads_per_workgroup(lib, dt, N):
         assert torch.equal(out, ref), f"{(out != ref).sum().item()} elements differ"
 
 
-@pytest.mark.parametrize("dt", ["fp16", "bf16"])
-@pytest.mark.parametrize("B,N,H", [(1, 257, 1), (37, 257, 16), (160, 257, 16), (5, 258, 4),
-                                   (2, 259, 2), (24, 259, 16), (3, 258, 7)])
-def test_attention_stream(exp_lib, dt, B, N, H):
-    """Streamed kernel (variant 9, experiments library): key tiles through an LDS
-    ring across a workgroup's heads (hpw 1..5 here). The 8 full query chunks run the x8
-    kernel's arithmetic in its order, so those rows equal variant 8's bit for
-    bit; the ragged rows 256.. (VALU partials, another summation order) agree
-    to rounding. Repeats must be identical (a ring race would vary)."""
-    lib = exp_lib
-    code, tdt = DT[dt]
-    g = torch.Generator(device="cuda").manual_seed(B * 1000 + N + H + 9)
-    qkv = (torch.randn(B * N, 3 * H * 64, device="cuda", generator=g) * 1.5).to(tdt)
-    ref8 = torch.empty(B * N, H * 64, device="cuda", dtype=tdt)
-    _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), ref8.data_ptr(), B, N, H, 64, 0, 8,
-                                        _stream()))
-    out = torch.empty_like(ref8)
-    first = None
-    for _ in range(3):
-        out.fill_(7.0)
-        _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), out.data_ptr(), B, N, H, 64, 0, 9,
-                                            _stream()))
-        torch.cuda.synchronize()
-        if first is None:
-            first = out.clone()
-        else:
-            assert torch.equal(out, first), f"{(out != first).sum().item()} elements vary"
-    ref = _attn_ref(qkv, B, N, H, 0)
-    err = (out.float() - ref).abs().max().item()
-    assert err < (4e-2 if dt == "bf16" else 6e-3), err
-    o3, r3 = out.view(B, N, -1), ref8.view(B, N, -1)
-    full = torch.equal(o3[:, :256], r3[:, :256])
-    assert full, f"{(o3[:, :256] != r3[:, :256]).sum().item()} full-chunk elements differ from variant 8"
-    rag = (o3[:, 256:].float() - r3[:, 256:].float()).abs().max().item()
-    assert rag < (1.6e-2 if dt == "bf16" else 2e-3), rag
-    for n, causal in ((256, 0), (260, 0), (200, 0), (257, 1)):
-        assert lib.miclip_op_attention(code, qkv.data_ptr(), out.data_ptr(), 1, n, H, 64, causal, 9,
-                                       _stream()) != 0
-
-
 def test_attention_spike(lib):
     """A key row that dominates one query forces the online-softmax rescale branch."""
     B, N, H = 1, 257, 1
@@ -410,41 +352,6 @@ def test_attention_dh80(lib, dt, B, N, H, causal):
     err = (out[:B * N].float() - ref).abs().max().item()
     assert err < (4e-2 if dt == "bf16" else 6e-3), err
     assert bool((out[B * N] == 7.0).all())
-
-
-@pytest.mark.parametrize("dt", ["fp16", "bf16"])
-@pytest.mark.parametrize("B,N,H", [(2, 577, 16), (3, 400, 4), (1, 608, 2), (2, 330, 3), (5, 257, 2),
-                                   (1, 128, 1)])
-def test_attention_two_phase_dh64_bitexact(lib, exp_lib, dt, B, N, H):
-    """The two-phase one-head-per-workgroup kernel (variant 3, experiments library:
-    measured level with attention_kernel<64>; first chunk's Q retired before the K/V
-    DMAs, key tiles [0, TA) computed while the rest lands) equals attention_kernel<64>
-    (variant 1) bit for bit, and fp32 SDPA within the kernel tolerance; the product
-    library refuses variant 3."""
-    code, tdt = DT[dt]
-    z = torch.zeros(N * 3 * 64, device="cuda", dtype=tdt)
-    assert lib.miclip_op_attention(code, z.data_ptr(), z.data_ptr(), 1, N, 1, 64, 0, 3,
-                                   _stream()) != 0
-    lib = exp_lib
-    g = torch.Generator(device="cuda").manual_seed(B * 1000 + N + H + 641)
-    qkv = (torch.randn(B * N, 3 * H * 64, device="cuda", generator=g) * 1.5).to(tdt)
-    outs = []
-    for v in (1, 3):
-        out = torch.full((B * N + 1, H * 64), 7.0, device="cuda", dtype=tdt)
-        _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), out.data_ptr(), B, N, H, 64, 0,
-                                            v, _stream()))
-        outs.append(out)
-    torch.cuda.synchronize()
-    for o in outs[1:]:
-        assert torch.equal(outs[0], o)
-    assert bool((outs[1][B * N] == 7.0).all())
-    ref = _attn_ref(qkv, B, N, H, False)
-    err = (outs[1][:B * N].float() - ref).abs().max().item()
-    assert err < (4e-2 if dt == "bf16" else 6e-3), err
-    x = torch.zeros(77, 3 * 64, device="cuda", dtype=tdt)   # causal: refused
-    y = torch.zeros(77, 64, device="cuda", dtype=tdt)
-    assert lib.miclip_op_attention(code, x.data_ptr(), y.data_ptr(), 1, 77, 1, 64, 1, 3,
-                                   _stream()) != 0
 
 
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])

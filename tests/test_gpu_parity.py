@@ -113,6 +113,15 @@ def test_encode_text_matches_reference(golden, tag, name, dtype):
     assert d1.max() <= COS_TOL and d2.max() <= COS_TOL
 
 
+def test_vitl14_336_text_golden_is_vitl14s(golden):
+    """test_encode_text_matches_reference skips vitl14_336 because its text tower is
+    ViT-L/14's (same text config and seeded weights): the two goldens must stay
+    byte-identical, or a regeneration could silently drop C4's text check."""
+    a, b = golden("vitl14"), golden("vitl14_336")
+    for key in ("tokens", "text_before", "text_proj", "text_weights"):
+        assert np.array_equal(a[key], b[key]), key
+
+
 @pytest.mark.parametrize("tag,name", CONFIGS)
 def test_zero_shot_top1(golden, tag, name):
     """Full chain on the GPU: encode_image -> proj -> normalize -> 100*f@W -> topk."""
@@ -214,6 +223,26 @@ def test_edge_batches():
         m.encode_text(torch.full((1, 77), 49408, dtype=torch.long))
 
 
+def test_runtime_toggles_survive_device_moves():
+    """set_cls_last / set_splits are runtime settings of the C handle; a device move
+    rebuilds the handle from the module, which must re-apply them (round-4 advice)."""
+    from miclip.weights import synthetic_images
+    m = _model("ViT-B/32", "fp16")
+    imgs = torch.from_numpy(synthetic_images(3, 224, seed=9)).cuda()
+    m.set_cls_last(False)
+    m.set_splits(1)
+    try:
+        full = m.encode_image(imgs)
+        m.cpu()
+        m.cuda()
+        assert not m.numerics()["cls_last"]
+        assert torch.equal(m.encode_image(imgs), full)
+    finally:
+        m.set_cls_last(True)
+        m.set_splits(2)
+    assert m.numerics()["cls_last"]
+
+
 def test_module_surface():
     m = _model("ViT-B/32", "fp16")
     sd = m.state_dict()
@@ -223,9 +252,11 @@ def test_module_surface():
     assert "visual.transformer.resblocks.11.mlp.c_proj.weight" in sd
 
 
-@pytest.mark.parametrize("B,C,k", [(13, 20, 5), (1, 7, 1), (64, 1000, 5)])
+@pytest.mark.parametrize("B,C,k", [(13, 20, 5), (1, 7, 1), (64, 1000, 5), (256, 1000, 10),
+                                   (17, 16, 16), (40, 33, 3)])
 def test_zero_shot_head_vs_torch(B, C, k):
-    """Batched head kernel (8 rows per workgroup, ragged tail) against torch fp32."""
+    """The head on the f32 MFMA (16 x 16 logits tiles, normalise fused; ragged rows and
+    classes) and the top-k kernel against torch fp32."""
     m = _model("ViT-B/32", "fp16")
     g = torch.Generator(device="cuda").manual_seed(B + C)
     feats = torch.randn(B, 768, device="cuda", generator=g)
@@ -261,6 +292,9 @@ def test_mxfp8_encode_within_fp8_tolerance(golden, tag, name):
     m = _model(name, "mxfp8")
     feats = m.encode_image(torch.from_numpy(imgs).cuda()).cpu()
     report(f"{tag}/mxfp8", feats, g["image"], MX_COS_TOL_IMAGE, MX_CENTRED_TOL_IMAGE)
+    nm = m.numerics()
+    # the MX vision tower is not LN-folded; the fp16 text tower is (round-4 advice)
+    assert nm["mxfp8"] and not nm["lnfold"] and nm["lnfold_text"]
     xb, xp = m.encode_text(torch.from_numpy(g["tokens"]).long().cuda())
     db = _one_minus_cos(xb.cpu(), g["text_before"])
     dt = _one_minus_cos(xp.cpu(), g["text_proj"])

@@ -94,15 +94,30 @@ def test_preprocess_shapes():
 
 
 def test_openclip_pretrained_rules():
-    """open_clip.create_model: a checkpoint tag raises (no checkpoints offline, and
-    seeded weights behind a real tag would be silent garbage); an unknown model
+    """open_clip.create_model: a checkpoint tag (no checkpoints offline) loads the
+    seeded weights with a SeededWeightsWarning -- never silently -- the same policy as
+    miclip.load(<model name>) (round-4 advice); an unknown model
     raises like open_clip; a state-dict file is checked against the NAMED config
     (ViT-H-14: GELU, 80-wide heads), which build_model's inference cannot see."""
     from types import SimpleNamespace
     from miclip import _checked_config
+    import miclip
     from miclip.openclip import create_model
-    with pytest.raises(RuntimeError, match="no pretrained checkpoints"):
-        create_model("ViT-H-14", pretrained="laion2b_s32b_b79k")
+    captured = {}
+
+    def fake_load(src, **kw):
+        captured.update(src=src, **kw)
+        raise RuntimeError("stop before the GPU")
+    real = miclip.load
+    miclip.load = fake_load
+    try:
+        for tag in ("openai", "laion2b_s32b_b79k"):
+            with pytest.warns(miclip.SeededWeightsWarning, match="SEEDED RANDOM"):
+                with pytest.raises(RuntimeError, match="stop before the GPU"):
+                    create_model("ViT-H-14", pretrained=tag, device="cpu")
+            assert captured["src"] == "ViT-H-14" and captured["config"] is None
+    finally:
+        miclip.load = real
     with pytest.raises(RuntimeError, match="not found"):
         create_model("ViT-Q-99")
     cfg = MODEL_CONFIGS["ViT-H-14"]
