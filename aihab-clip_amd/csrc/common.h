@@ -122,6 +122,61 @@ MICLIP_DEV float wave_sum(float v) {
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// DPP lane move within a 16-lane row (bound_ctrl: lanes with no source read 0)
+template <int CTRL>
+MICLIP_DEV float dppf(float x) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
+}
+
+// Sum over the 32 lanes of a half-wave: DPP (quad_perm, row_half_mirror,
+// row_mirror) within each 16-lane row, then v_permlane16_swap (rows 0<->1,
+// 2<->3) for the last step -- no LDS round trip; every lane of the half gets the
+// same value (row 0's + row 1's partial, in that order, on both rows).
+MICLIP_DEV float half_sum(float x) {
+  x += dppf<0xB1>(x);    // quad_perm [1,0,3,2]
+  x += dppf<0x4E>(x);    // quad_perm [2,3,0,1]
+  x += dppf<0x141>(x);   // row_half_mirror (lane i <-> 7-i of its 8)
+  x += dppf<0x140>(x);   // row_mirror (lane i <-> 15-i of its 16)
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(a[0]) + __uint_as_float(a[1]);
+}
+
+// LayerNorm statistics of the fp16 residual stream in 256-column slices (the
+// folded LayerNorm's {mean, rstd}, clip/model.py:151-157): a half-wave holds one
+// row's slice, lane l (of 32) its columns 8l .. 8l+7 as 4 fp16 pairs. Two-pass
+// over the slice: mean = sum / 256, M2 = sum (x - mean)^2, returned as
+// {mean, M2} on every lane of the half. The fp16 residual GEMM epilogue emits
+// these partials for the rows it writes and ln_stats_kernel computes them for
+// any other row with this same function, so a row's statistics are bit-identical
+// whichever kernel produced its partials (batch invariance). Explicit fmaf: no
+// contraction choice is left to the compiler.
+typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+MICLIP_DEV float2 slice_stats(const unsigned (&w)[4]) {
+  // the lane's sum by v_dot2_f32_f16 against (1, 1): fp16 pairs into fp32
+  const h2_t one = {(_Float16)1.0f, (_Float16)1.0f};
+  const float s = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, w[0]), one,
+                                         __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, w[1]), one, 0.f, false),
+                                         false) +
+                  __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, w[2]), one,
+                                         __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, w[3]), one, 0.f, false),
+                                         false);
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[2 * e] = (float)__builtin_bit_cast(_Float16, (unsigned short)(w[e] & 0xffffu));
+    v[2 * e + 1] = (float)__builtin_bit_cast(_Float16, (unsigned short)(w[e] >> 16));
+  }
+  const float mean = half_sum(s) * (1.0f / 256.0f);
+  float q = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float d = v[e] - mean;
+    q = __builtin_fmaf(d, d, q);
+  }
+  return make_float2(mean, half_sum(q));
+}
+
 MICLIP_DEV float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -8,12 +8,6 @@ namespace miclip {
 
 namespace {
 
-template <int CTRL>
-MICLIP_DEV float dppf(float x) {
-  return __builtin_bit_cast(
-      float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
-}
-
 // max over the 8 consecutive lanes of a 32-element block (4 elements per lane)
 MICLIP_DEV float block8_max(float m) {
   m = fmaxf(m, dppf<0xB1>(m));    // quad_perm [1,0,3,2]
