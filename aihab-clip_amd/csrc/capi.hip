@@ -100,10 +100,6 @@ struct Workspace {
   float* feat = nullptr;  // [items, W] fp32 scratch
   int32_t* rows = nullptr;
   float* stats = nullptr;  // [rows] {mean, rstd} for the folded LayerNorm
-  // [rows, W / 256] LayerNorm slice partials written by the last fp16 residual GEMM
-  // (gemm_residual part) for its first `covered` rows; ln_stats merges them
-  float* part = nullptr;
-  int covered = 0;
 };
 
 }  // namespace
@@ -297,7 +293,7 @@ int ensure_ws(miclip_model* m, Workspace& w, int items, int ntok, int W, bool im
   // grow: make sure no queued kernel still uses the old buffers
   MICLIP_HIP(hipDeviceSynchronize());
   for (void* p : {w.patches, (void*)w.x, w.h, w.qkv, w.o, w.f, w.hq, w.hs, w.fq, w.fs, w.xc,
-                  (void*)w.feat, (void*)w.rows, (void*)w.stats, (void*)w.part})
+                  (void*)w.feat, (void*)w.rows, (void*)w.stats})
     dev_free(m, p);
   w = Workspace{};
   int rc;
@@ -323,7 +319,6 @@ int ensure_ws(miclip_model* m, Workspace& w, int items, int ntok, int W, bool im
   if ((rc = dev_alloc(m, (void**)&w.feat, (size_t)items * W * 4))) return rc;
   if ((rc = dev_alloc(m, (void**)&w.rows, (size_t)items * 4))) return rc;
   if ((rc = dev_alloc(m, (void**)&w.stats, (size_t)rows * 8))) return rc;
-  if (m->lnfold && (rc = dev_alloc(m, (void**)&w.part, (size_t)rows * (W / 256) * 8))) return rc;
   w.cap_items = items;
   w.cap_rows = rows;
   return 0;
@@ -399,10 +394,8 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
   const bool mx = b.s_qkv != nullptr;   // MX-fp8 operands for QKV / c_fc / c_proj (vision)
   const bool fold = m->lnfold && b.wf_qkv;
   if (fold) {
-    // rows the previous residual GEMM covered: 32 B of partials per row, not x
-    const double dR = dM - w.covered;
-    ProfScope p(m, K_LAYERNORM, s, 0, dR * dW * rb + w.covered * (dW / 256) * 8 + dM * 8);
-    MICLIP_HIP(ln_stats(w.x, w.stats, M, W, s, b.fs_qkv, w.part, w.covered));
+    ProfScope p(m, K_LAYERNORM, s, 0, dM * (dW * rb + 8));
+    MICLIP_HIP(ln_stats(w.x, w.stats, M, W, s, b.fs_qkv));
   } else {
     ProfScope p(m, K_LAYERNORM, s, 0, dM * dW * (rb + (mx ? 1 : 2)));
     if (mx)
@@ -480,14 +473,12 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
       MICLIP_HIP(gemm_mx(w.hq, w.hs, b.w_out, b.s_out, b.b_out, w.x, nullptr, M, W, W, 1,
                          ACT_NONE, s, m->gemm_variant[2]));
     } else {
-      MICLIP_HIP(gemm_residual(dt, w.o, b.w_out, b.b_out, w.x, M, W, W, s, r16 ? vres : 0, r16,
-                               nullptr, 1, fold ? w.part : nullptr, &w.covered));
+      MICLIP_HIP(gemm_residual(dt, w.o, b.w_out, b.b_out, w.x, M, W, W, s, r16 ? vres : 0, r16));
     }
   }
   if (fold) {
-    const double dR = dM - w.covered;
-    ProfScope p(m, K_LAYERNORM, s, 0, dR * dW * rb + w.covered * (dW / 256) * 8 + dM * 8);
-    MICLIP_HIP(ln_stats(w.x, w.stats, M, W, s, b.fs_fc, w.part, w.covered));
+    ProfScope p(m, K_LAYERNORM, s, 0, dM * (dW * rb + 8));
+    MICLIP_HIP(ln_stats(w.x, w.stats, M, W, s, b.fs_fc));
   } else {
     ProfScope p(m, K_LAYERNORM, s, 0, dM * dW * (rb + (mx ? 1 : 2)));
     if (mx)
@@ -518,7 +509,7 @@ int run_block(miclip_model* m, const Block& b, Workspace& w, int items, int N, i
                          ACT_NONE, s, m->gemm_variant[2]));
     else
       MICLIP_HIP(gemm_residual(dt, w.f, b.w_proj, b.b_proj, w.x, M, W, 4 * W, s, r16 ? vres : 0,
-                               r16, nullptr, 1, m->lnfold ? w.part : nullptr, &w.covered));
+                               r16));
   }
   return 0;
 }
@@ -548,8 +539,6 @@ Workspace view(const miclip_model* m, const Workspace& w, size_t row0, size_t it
   v.feat = w.feat + item0 * W;
   v.rows = w.rows + item0;
   v.stats = w.stats + 2 * row0;
-  if (w.part) v.part = w.part + 2 * row0 * (W / 256);
-  v.covered = 0;
   (void)N;
   return v;
 }
@@ -593,7 +582,6 @@ int encode_image_part(miclip_model* m, Workspace w, const void* images, int in_d
                          m->resid16 ? nullptr : (float*)w.x, m->resid16 ? w.x : nullptr, M, W,
                          0, s, m->resid16));
   }
-  w.covered = 0;   // x was written by ln_pre: no LN partials
   // the last block on the CLS rows only (run_block); N beyond attention_q0's
   // range (never for CLIP's towers) runs it whole
   const bool cls_last = m->cls_last && N <= 768;
@@ -945,7 +933,6 @@ int miclip_encode_text(miclip_model* m, const int64_t* tokens, int32_t P, float*
     MICLIP_HIP(token_embed(tokens, m->tok_emb, m->tpos, w.x, w.rows, P, L, W, c.vocab_size, s,
                            m->resid16));
   }
-  w.covered = 0;   // x was written by token_embed: no LN partials
   for (int l = 0; l < c.transformer_layers; ++l)
     if ((rc = run_block(m, m->tblocks[l], w, P, L, W, H, 64, 1, s))) return rc;
   float* xb = x_before ? x_before : w.feat;
@@ -1167,24 +1154,6 @@ int miclip_op_ln_stats(const void* x, float* stats, int32_t R, int32_t D, const 
                        void* stream) {
   if (!x || !stats) return fail(MICLIP_EINVAL, "null argument");
   MICLIP_HIP(ln_stats(x, stats, R, D, (hipStream_t)stream, rscale));
-  return 0;
-}
-
-int miclip_op_gemm_residual_part(int32_t dtype, const void* A, const void* W, const float* bias,
-                                 void* X, int32_t M, int32_t N, int32_t K, float* part,
-                                 int32_t* covered, int32_t variant, void* stream) {
-  if (!A || !W || !bias || !X || !part || !covered) return fail(MICLIP_EINVAL, "null argument");
-  int cov = 0;
-  MICLIP_HIP(gemm_residual(dtype, A, W, bias, X, M, N, K, (hipStream_t)stream, variant, 1,
-                           nullptr, 1, part, &cov));
-  *covered = cov;
-  return 0;
-}
-
-int miclip_op_ln_stats_part(const void* x, const float* part, int32_t covered, float* stats,
-                            int32_t R, int32_t D, const float* rscale, void* stream) {
-  if (!x || !stats || (covered > 0 && !part)) return fail(MICLIP_EINVAL, "null argument");
-  MICLIP_HIP(ln_stats(x, stats, R, D, (hipStream_t)stream, rscale, part, covered));
   return 0;
 }
 

@@ -142,41 +142,6 @@ MICLIP_DEV float half_sum(float x) {
   return __uint_as_float(a[0]) + __uint_as_float(a[1]);
 }
 
-// LayerNorm statistics of the fp16 residual stream in 256-column slices (the
-// folded LayerNorm's {mean, rstd}, clip/model.py:151-157): a half-wave holds one
-// row's slice, lane l (of 32) its columns 8l .. 8l+7 as 4 fp16 pairs. Two-pass
-// over the slice: mean = sum / 256, M2 = sum (x - mean)^2, returned as
-// {mean, M2} on every lane of the half. The fp16 residual GEMM epilogue emits
-// these partials for the rows it writes and ln_stats_kernel computes them for
-// any other row with this same function, so a row's statistics are bit-identical
-// whichever kernel produced its partials (batch invariance). Explicit fmaf: no
-// contraction choice is left to the compiler.
-typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
-MICLIP_DEV float2 slice_stats(const unsigned (&w)[4]) {
-  // the lane's sum by v_dot2_f32_f16 against (1, 1): fp16 pairs into fp32
-  const h2_t one = {(_Float16)1.0f, (_Float16)1.0f};
-  const float s = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, w[0]), one,
-                                         __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, w[1]), one, 0.f, false),
-                                         false) +
-                  __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, w[2]), one,
-                                         __builtin_amdgcn_fdot2(__builtin_bit_cast(h2_t, w[3]), one, 0.f, false),
-                                         false);
-  float v[8];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    v[2 * e] = (float)__builtin_bit_cast(_Float16, (unsigned short)(w[e] & 0xffffu));
-    v[2 * e + 1] = (float)__builtin_bit_cast(_Float16, (unsigned short)(w[e] >> 16));
-  }
-  const float mean = half_sum(s) * (1.0f / 256.0f);
-  float q = 0.f;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float d = v[e] - mean;
-    q = __builtin_fmaf(d, d, q);
-  }
-  return make_float2(mean, half_sum(q));
-}
-
 MICLIP_DEV float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -287,11 +287,6 @@ struct EpiResidual {
   R* X;
   const float* bias;
   int ldx;
-  // fp16 stream (nullable): the LayerNorm slice partials {mean, M2} of the rows
-  // written, [rows, ldx / 256] float2 (slice_stats, common.h), emitted by the
-  // persistent kernel's transposed-accumulator readback for the next folded GEMM's
-  // ln_stats (which computes any row not covered itself, with the same function)
-  float2* part = nullptr;
   MICLIP_DEV float4 bias4(int col) const { return ld_bias4(bias, col); }
   MICLIP_DEV float4 bias4nb(int col) const { return ld_bias4_nb(bias, col); }
   MICLIP_DEV float bias1(int col) const { return bias[col]; }

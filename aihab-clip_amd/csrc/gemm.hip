@@ -885,10 +885,7 @@ MICLIP_DEV void wait_vmcnt_tile(int n) {
   switch (n) {
     case 36: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
     case 32: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
-    case 30: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
     case 28: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
-    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-    case 23: asm volatile("s_waitcnt vmcnt(23)" ::: "memory"); break;
     case 22: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); break;
     case 21: asm volatile("s_waitcnt vmcnt(21)" ::: "memory"); break;
     case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
@@ -1276,10 +1273,6 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
         // stores, each half-wave writing one whole 512-B row segment.
         const int h = lane >> 5, li = lane & 31;
         auto* cb = tr_out(epi) + cn0 + li * 8;
-        // fp16 residual: the LayerNorm slice partials of the rows written
-        // (slice_stats on the final x row pieces); lane li of each half keeps row
-        // pair li's and stores it after the pass (one store instruction per pass)
-        float2 keep = make_float2(0.f, 0.f);
 #pragma unroll
         for (int p0 = 0; p0 < RPW / 2; p0 += 2) {
           i16x4 va[2], vb[2];
@@ -1302,25 +1295,9 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
               Epi::template add_x<4>(t, x);
               w = (u32x4){t[0], t[1], t[2], t[3]};
             }
-            if constexpr (PrefetchX<Epi>::value) xq[p0 + p] = w;   // the final x piece
             const int ir = wave * RPW + 2 * (p0 + p) + h;
             const int row = cm0 + (ir / QR) * SR + qi * QR + (ir % QR);
             if (full || row < M) *(u32x4*)(cb + (size_t)row * tr_ld(epi)) = w;
-          }
-        }
-        if constexpr (PrefetchX<Epi>::value) {
-          if (epi.part) {   // kernel argument: wave-uniform
-            // after the pass's stores: RPW / 2 independent chains (latency hidden)
-#pragma unroll
-            for (int k = 0; k < RPW / 2; ++k) {
-              const unsigned wv[4] = {xq[k][0], xq[k][1], xq[k][2], xq[k][3]};
-              const float2 st = slice_stats(wv);
-              if (li == k) keep = st;
-            }
-            const int ir = wave * RPW + 2 * li + h;
-            const int row = cm0 + (ir / QR) * SR + qi * QR + (ir % QR);
-            if (li < RPW / 2 && (full || row < M))
-              epi.part[(size_t)row * (epi.ldx >> 8) + (cn0 >> 8)] = keep;
           }
         }
         MICLIP_STAMP(7);              // readback + store issue
@@ -1444,10 +1421,7 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
     }
     lds_barrier();                 // staging (buffer-1 half) free for the next tile
     // RB 3: 12 rows per wave and pass instead of 16 (TR epilogues only)
-    // (+ the 2 partials stores, one per pass, of the fp16 residual's LN partials)
-    int part_stores = 0;
-    if constexpr (TR && PrefetchX<Epi>::value) part_stores = epi.part ? 2 : 0;
-    prev_stores = full ? EpiStores<Epi, TR>::n * RB / 4 + part_stores : 0;
+    prev_stores = full ? EpiStores<Epi, TR>::n * RB / 4 : 0;
     MICLIP_STAMP(3);              // epilogue
   }
   // the row tail on the same workgroups
@@ -1737,19 +1711,8 @@ bool gemm_shape_ok(int M, int N, int K) {
 
 template <typename T, class Epi>
 hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hipStream_t s,
-                  int variant = 0, float* skws = nullptr, int sk = 1, int* covered = nullptr) {
-  if (covered) *covered = 0;
+                  int variant = 0, float* skws = nullptr, int sk = 1) {
   if (!gemm_shape_ok(M, N, K)) return hipErrorInvalidValue;
-  // rows whose LN slice partials the launch writes (fp16 residual, epi.part): those
-  // of the transposed-accumulator persistent kernel's data-parallel tiles
-  auto cover = [&](int rows) {
-    if constexpr (PrefetchX<Epi>::value) {
-      if (covered && epi.part) *covered = rows < M ? rows : M;
-    }
-  };
-  if constexpr (PrefetchX<Epi>::value) {
-    if (!covered) epi.part = nullptr;
-  }
   if (sk > 1) {   // split-K (small M, long K: the CLS-only last block), deterministic
     if (!skws || K % (sk * BK) || N % 128) return hipErrorInvalidValue;
     const int tiles = ((M + 127) / 128) * (N / 128);
@@ -1796,7 +1759,6 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
         hipLaunchKernelGGL((gemm256s_kernel<T, Epi, true, 0, 3>), dim3(t192 < ncu ? t192 : ncu),
                            dim3(512), 0, s, (const T*)A, (const T*)W, M, N, K, epi, gm, ntm3, 0,
                            0);
-        cover(M);   // no row tail: every row is in a tile
         return hipGetLastError();
       }
     }
@@ -1808,7 +1770,6 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
     const int ndp = tp.ntm_dp * (N / 256), ncu = cu_count();
     const int grid = ndp < ncu ? ndp : ncu;
     if constexpr (TrAcc<Epi>::value) {
-      if (!variant_tracc_off && diag == 0) cover(tp.ntm_dp * 256);   // the tail rows: ln_stats
       if (variant_tracc_off) {
         hipLaunchKernelGGL((gemm256s_kernel<T, Epi, false>), dim3(grid), dim3(512), 0, s,
                            (const T*)A, (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs,
@@ -1947,13 +1908,13 @@ hipError_t gemm_store_ln(int dtype, const void* A, const void* W, const float* c
 
 hipError_t gemm_residual(int dtype, const void* A, const void* W, const float* bias, void* X,
                          int M, int N, int K, hipStream_t s, int v, int resid16, float* skws,
-                         int sk, void* part, int* covered) {
-  if (covered) *covered = 0;
+                         int sk) {
   if (resid16) {  // fp16 residual stream (fp16 or bf16 operands)
-    if (part && N % 256) return hipErrorInvalidValue;
-    const EpiResidual<_Float16> epi{(_Float16*)X, bias, N, (float2*)part};
-    if (dtype == kBF16) return launch<__bf16>(A, W, M, N, K, epi, s, v, skws, sk, covered);
-    return launch<_Float16>(A, W, M, N, K, epi, s, v, skws, sk, covered);
+    if (dtype == kBF16)
+      return launch<__bf16>(A, W, M, N, K, EpiResidual<_Float16>{(_Float16*)X, bias, N}, s, v,
+                            skws, sk);
+    return launch<_Float16>(A, W, M, N, K, EpiResidual<_Float16>{(_Float16*)X, bias, N}, s, v,
+                            skws, sk);
   }
   if (dtype == kF16)
     return launch<_Float16>(A, W, M, N, K, EpiResidual<float>{(float*)X, bias, N}, s, v, skws,

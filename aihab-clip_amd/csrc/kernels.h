@@ -32,14 +32,9 @@ hipError_t gemm_store_ln(int dtype, const void* A, const void* W, const float* c
                          int sk = 1);
 // Residual epilogue: X (ld = N) += acc + bias; X fp32, or fp16 when resid16
 // (fp16 compute only: the reference's fp16 GPU residual stream).
-// part / covered (fp16 stream, nullable): the kernel may also write the LayerNorm
-// slice partials of the rows it produces (part [M, N/256] float2, slice_stats), and
-// *covered receives how many leading rows have them (0: none; ln_stats computes the
-// rest).
 hipError_t gemm_residual(int dtype, const void* A, const void* W, const float* bias, void* X,
                          int M, int N, int K, hipStream_t s, int variant = 0, int resid16 = 0,
-                         float* skws = nullptr, int sk = 1, void* part = nullptr,
-                         int* covered = nullptr);
+                         float* skws = nullptr, int sk = 1);
 // Float epilogue: C (fp32, ld = N) = acc + bias (bias may be null).
 hipError_t gemm_f32(int dtype, const void* A, const void* W, const float* bias, float* C,
                     int M, int N, int K, hipStream_t s, int variant = 0);
@@ -80,14 +75,10 @@ hipError_t layernorm(int dtype, const void* in, const int32_t* rows, int in_stri
                      void* out_q = nullptr, void* out_s = nullptr);
 
 // Row statistics of the fp16 residual stream for the folded LayerNorm: stats[r] =
-// {mean, rstd * *rscale} of row r of in [R, D] (fp32, eps 1e-5), merged from 256-column
-// slice partials {mean, M2} (slice_stats, common.h); rows r < covered take theirs from
-// part [R, D/256] float2 (the fp16 residual GEMM's, gemm_residual), the others are
-// computed from in -- the same bits either way. rscale (device, nullable = 1) is the
-// weight's 1/S from ln_fold.
+// {mean, rstd * *rscale} of row r of in [R, D], mean and rstd exactly as layernorm
+// computes them; rscale (device, nullable = 1) is the weight's 1/S from ln_fold.
 hipError_t ln_stats(const void* in, float* stats, int R, int D, hipStream_t s,
-                    const float* rscale = nullptr, const void* part = nullptr,
-                    int covered = 0);
+                    const float* rscale = nullptr);
 // Fold LayerNorm (gamma, beta) into the following Linear (W [N, K] compute dtype,
 // bias [N] fp32 or null): Wf = W diag(gamma) * S (compute dtype), colsum[j] = sum_k Wf[j,k],
 // c[j] = bias[j] + sum_k beta[k] W[j,k] (sums in double, fixed order). S is the power

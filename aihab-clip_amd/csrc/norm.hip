@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const TI* in,  // may al
 // per-block ln_1 / ln_2 and in-place ln_pre): two rows per wave, a half-wave
 // per row, 8 values per lane per 256 columns, so every load and store is 16 B
 // (the general kernel moves 8 B per lane for fp16). Sums over the 32 lanes of
-// a half-wave: half_sum (common.h).
+// a half-wave: half_sum (common.h; DPP, then v_permlane16_swap for the last step).
 
 // MX = true: MX-fp8 output (the fp8 GEMM's A operand) instead of T; a 32-value
 // block is the 4 lanes of a quad here (8 values per lane), scale by lane 0 of it.
@@ -193,62 +193,40 @@ __global__ __launch_bounds__(256) void layernorm_h2_kernel(const _Float16* in,  
   }
 }
 
-// Statistics only (folded LayerNorm, epilogue.h EpiStoreLN): {mean, rstd} per
-// row from 256-column slice partials {mean, M2} (slice_stats, common.h) merged
-// in column order by Chan's rule (merge_stats). Rows below `covered` take their
-// partials from `part` ([R, NI] float2, written by the fp16 residual GEMM that
-// produced them, gemm.hip): one thread per row, 32 contiguous bytes each. The
-// others are computed here from x with the same slice_stats (a half-wave per row,
-// 16-B loads), so every row's statistics are the same bits whichever path
-// produced it. rscale (nullable): the folded weight's 1/S (ln_fold), a power of
-// two, so {mean, rstd / S} is exact and the GEMM epilogue needs no extra multiply.
-template <int NI>
-MICLIP_DEV float2 merge_stats(const float2 (&ps)[NI], const float* rscale) {
-  float mean = ps[0].x, m2 = ps[0].y;
-#pragma unroll
-  for (int i = 1; i < NI; ++i) {   // n_a = 256 i columns so far, n_b = 256
-    const float d = ps[i].x - mean;
-    mean = __builtin_fmaf(d, 1.0f / (float)(i + 1), mean);
-    m2 = __builtin_fmaf(d * d, 256.0f * (float)i / (float)(i + 1), m2 + ps[i].y);
-  }
-  const float rstd = rsqrtf(m2 / (float)(NI * 256) + 1e-5f);
-  return make_float2(mean, rscale ? rstd * *rscale : rstd);
-}
-
-// blocks [0, ncov): rows [0, covered), a thread per row; blocks [ncov, ...): rows
-// [covered, R), a half-wave per row
+// Statistics only (folded LayerNorm, epilogue.h EpiStoreLN): the same rows per
+// wave, loads and reductions as layernorm_h2_kernel, so {mean, rstd} are the
+// values that kernel normalises with; one 8-byte store per row.
+// rscale (nullable): the folded weight's 1/S (ln_fold), a power of two, so
+// {mean, rstd / S} is exact and the GEMM epilogue needs no extra multiply.
 template <int NI>
 __global__ __launch_bounds__(256) void ln_stats_kernel(const _Float16* __restrict__ in,
-                                                       const float2* __restrict__ part,
-                                                       int covered, int ncov,
-                                                       float2* __restrict__ stats, int R,
+                                                       float2* __restrict__ stats, int R, int D,
                                                        const float* __restrict__ rscale) {
-  constexpr int D = NI * 256;
-  if ((int)blockIdx.x < ncov) {
-    const int r = blockIdx.x * 256 + threadIdx.x;
-    if (r >= covered) return;
-    float2 ps[NI];
-#pragma unroll
-    for (int i = 0; i < NI; ++i) ps[i] = part[(size_t)r * NI + i];
-    stats[r] = merge_stats<NI>(ps, rscale);
-    return;
-  }
   const int lane = threadIdx.x & 63, hl = lane & 31;
-  const int r0 = covered + ((blockIdx.x - ncov) * 4 + (threadIdx.x >> 6)) * 2;
-  if (r0 >= R) return;   // wave-uniform
-  const int r = r0 + (lane >> 5);
+  const int r = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  if ((blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 >= R) return;
   const bool valid = r < R;
   const _Float16* src = in + (size_t)(valid ? r : R - 1) * D + hl * 8;
-  u32x4 h[NI];
-#pragma unroll
-  for (int i = 0; i < NI; ++i) h[i] = *(const u32x4*)(src + i * 256);
-  float2 ps[NI];
+  float v[NI][8];
+  float s = 0.f;
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
-    const unsigned w[4] = {h[i][0], h[i][1], h[i][2], h[i][3]};
-    ps[i] = slice_stats(w);
+    const i16x8 h = *(const i16x8*)(src + i * 256);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[i][e] = from_bits<_Float16>(h[e]);
+    s += ((v[i][0] + v[i][1]) + (v[i][2] + v[i][3])) + ((v[i][4] + v[i][5]) + (v[i][6] + v[i][7]));
   }
-  if (valid && hl == 0) stats[r] = merge_stats<NI>(ps, rscale);
+  const float mean = half_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = v[i][e] - mean;
+      q += d * d;
+    }
+  const float rstd = rsqrtf(half_sum(q) / (float)D + 1e-5f);
+  if (valid && hl == 0) stats[r] = make_float2(mean, rscale ? rstd * *rscale : rstd);
 }
 
 // max |W[j,k] * gamma[k]| over the matrix, as the bits of a non-negative float
@@ -377,16 +355,13 @@ hipError_t ln_dispatch(const TI* in, const int32_t* rows, int stride, const floa
 }  // namespace
 
 hipError_t ln_stats(const void* in, float* stats, int R, int D, hipStream_t s,
-                    const float* rscale, const void* part, int covered) {
-  if (R < 1 || D % 256 || D > 1536 || !in || !stats || (covered > 0 && !part))
-    return hipErrorInvalidValue;
-  const int cov = part ? (covered < R ? covered : R) : 0;
-  const int ncov = (cov + 255) / 256;
-  const dim3 grid(ncov + (R - cov + 7) / 8), block(256);
-#define MICLIP_LNS_CASE(V)                                                               \
-  case V:                                                                                \
-    hipLaunchKernelGGL((ln_stats_kernel<V>), grid, block, 0, s, (const _Float16*)in,     \
-                       (const float2*)part, cov, ncov, (float2*)stats, R, rscale);        \
+                    const float* rscale) {
+  if (R < 1 || D % 256 || D > 1536 || !in || !stats) return hipErrorInvalidValue;
+  const dim3 grid((R + 7) / 8), block(256);
+#define MICLIP_LNS_CASE(V)                                                              \
+  case V:                                                                               \
+    hipLaunchKernelGGL((ln_stats_kernel<V>), grid, block, 0, s, (const _Float16*)in,    \
+                       (float2*)stats, R, D, rscale);                                   \
     break;
   switch (D / 256) {
     MICLIP_LNS_CASE(1)

@@ -322,17 +322,6 @@ int miclip_op_gemm_splitk(int32_t dtype, const void* A, const void* W, const flo
                           float* ws, void* stream);
 int miclip_op_ln_stats(const void* x, float* stats, int32_t R, int32_t D, const float* rscale,
                        void* stream);
-/* The fp16 residual GEMM that also emits the folded LayerNorm's slice partials
- * (miclip_op_gemm epi 4, plus part [M, N/256] float2 {mean, M2} per 256-column
- * slice of the rows it writes); *covered (host) receives how many leading rows
- * have partials (0 where the launch runs a kernel without them).
- * miclip_op_ln_stats_part: miclip_op_ln_stats taking rows < covered from part --
- * the same bits as computing them from x (the partials' batch invariance). */
-int miclip_op_gemm_residual_part(int32_t dtype, const void* A, const void* W, const float* bias,
-                                 void* X, int32_t M, int32_t N, int32_t K, float* part,
-                                 int32_t* covered, int32_t variant, void* stream);
-int miclip_op_ln_stats_part(const void* x, const float* part, int32_t covered, float* stats,
-                            int32_t R, int32_t D, const float* rscale, void* stream);
 int miclip_op_ln_fold(int32_t dtype, const void* W, const float* gamma, const float* beta,
                       const float* bias, void* Wf, float* colsum, float* c, int32_t N, int32_t K,
                       float* inv_scale, void* stream);

@@ -246,49 +246,3 @@ def test_benched_config_vitl14_bs256(golden):
     assert all(same)
     again = m.encode_image(torch.from_numpy(batch).cuda()).cpu()
     assert torch.equal(feats, again), "bs=256 encode is not deterministic"
-
-
-@pytest.mark.parametrize("M,N,K", [(65792, 1024, 1024), (32896, 1024, 4096), (12800, 768, 3072),
-                                   (16421, 1024, 1024), (1000, 1024, 1024), (50, 768, 768)])
-def test_residual_ln_partials_bitexact(lib, M, N, K):
-    """The fp16 residual GEMM's LayerNorm slice partials (out-proj / c_proj epilogue,
-    round 5): x is unchanged by emitting them (same bits as miclip_op_gemm epi 4), and
-    the statistics merged from them equal, bit for bit, the statistics ln_stats
-    computes from x alone -- the same slice_stats arithmetic -- so a row's {mean, rstd}
-    does not depend on which kernel (tile, row tail, 128x128) wrote it. Large M
-    covers the persistent kernel's rows (the row tail: ln_stats); small M none."""
-    g = torch.Generator(device="cuda").manual_seed(M + N + K)
-    A = (torch.randn(M, K, device="cuda", generator=g) * 0.5).half()
-    W = (torch.randn(N, K, device="cuda", generator=g) * K ** -0.5).half()
-    bias = 0.1 * torch.randn(N, device="cuda", generator=g)
-    x0 = _stream_rows(M, N, g)
-    ref = x0.clone()
-    _check(lib, lib.miclip_op_gemm(0, A.data_ptr(), W.data_ptr(), bias.data_ptr(), ref.data_ptr(),
-                                   M, N, K, 4, 0, 0, _stream()))
-    x = x0.clone()
-    part = torch.full((M, N // 256, 2), float("nan"), device="cuda")
-    cov = ctypes.c_int32(-1)
-    _check(lib, lib.miclip_op_gemm_residual_part(0, A.data_ptr(), W.data_ptr(), bias.data_ptr(),
-                                                 x.data_ptr(), M, N, K, part.data_ptr(),
-                                                 ctypes.byref(cov), 0, _stream()))
-    torch.cuda.synchronize()
-    assert torch.equal(x, ref)
-    covered = cov.value
-    if M >= 12800:
-        assert covered >= M - 256 and covered % 64 == 0, covered
-    assert 0 <= covered <= M
-    assert not torch.isnan(part[:covered]).any()
-    st_part = torch.empty(M, 2, device="cuda")
-    st_x = torch.empty(M, 2, device="cuda")
-    sc = torch.tensor([0.25, 0.0], device="cuda")
-    _check(lib, lib.miclip_op_ln_stats_part(x.data_ptr(), part.data_ptr(), covered,
-                                            st_part.data_ptr(), M, N, sc.data_ptr(), _stream()))
-    _check(lib, lib.miclip_op_ln_stats_part(x.data_ptr(), None, 0, st_x.data_ptr(), M, N,
-                                            sc.data_ptr(), _stream()))
-    torch.cuda.synchronize()
-    assert torch.equal(st_part, st_x), f"{(st_part != st_x).any(1).sum().item()} rows differ"
-    xd = x.double()
-    mu = xd.mean(1)
-    rstd = 0.25 / torch.sqrt(((xd - mu[:, None]) ** 2).mean(1) + 1e-5)
-    assert ((st_x[:, 0].double() - mu).abs() / mu.abs()).max().item() < 1e-6
-    assert ((st_x[:, 1].double() - rstd) / rstd).abs().max().item() < 1e-4
