@@ -38,7 +38,18 @@ stamps: $(OBJS)
 	$(HIPCC) $(HIPFLAGS) -c scripts/stamps/stamp_gemm_kloop.hip -o build/stamps/stamp_gemm_kloop.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) build/stamps/stamp_gemm_kloop.o $(filter-out $(OBJ_DIR)/gemm.o,$(OBJS)) -o build/stamps/libstamp_gemm_kloop.so
 
+# timing diagnostics (outputs meaningless): the library without the vision-tower
+# attention / without the large ln_stats launches, to price what each costs inside
+# the two-stream step (bench.py with MICLIP_LIB=build/diag/libmiclip_<x>.so)
+DIAG_DIR := build/diag
+diag: $(OBJS)
+	@mkdir -p $(DIAG_DIR)
+	$(HIPCC) $(HIPFLAGS) -fno-honor-nans -fno-slp-vectorize -DMICLIP_DIAG_SKIP_ATTN -c $(SRC_DIR)/attention.hip -o $(DIAG_DIR)/attention_noattn.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(DIAG_DIR)/attention_noattn.o $(filter-out $(OBJ_DIR)/attention.o,$(OBJS)) -o $(DIAG_DIR)/libmiclip_noattn.so
+	$(HIPCC) $(HIPFLAGS) -DMICLIP_DIAG_SKIP_LNSTATS -c $(SRC_DIR)/norm.hip -o $(DIAG_DIR)/norm_nolns.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(DIAG_DIR)/norm_nolns.o $(filter-out $(OBJ_DIR)/norm.o,$(OBJS)) -o $(DIAG_DIR)/libmiclip_nolns.so
+
 clean:
 	rm -rf build $(LIB)
 
-.PHONY: all clean asm stamps
+.PHONY: all clean asm stamps diag

@@ -204,6 +204,10 @@ MICLIP_DEV i16x4 ds_read_tr16_b64(const void* lds) {
   return __builtin_bit_cast(
       i16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4_vs*)(lds)));
 }
+MICLIP_DEV i16x4 ds_read_tr16_b64(const LDS_AS char* lds) {
+  return __builtin_bit_cast(
+      i16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS i16x4_vs*)(lds)));
+}
 
 // Bijective XCD-aware block remap (cdna_hip_programming.md §5.5 T1): blocks that
 // the dispatcher deals to one XCD (b, b+8, ...) get a contiguous range of tiles.
