@@ -119,13 +119,12 @@ MICLIP_DEV float dot2acc<__bf16>(uint32_t a, uint32_t b, float c) {
 // and O^T (cdna_hip_programming.md T13: the decision precedes the tile's
 // exponentials; the old max is kept while the tile max exceeds it by <= 8, p <=
 // 2^8, exact range for fp16/bf16 P). Leaves P^T as the P.V MFMA's B operand
-// (pf[s2]: accumulator regs 8 s2 .. 8 s2 + 7) and, for DH 64, adds the row sum
-// of that rounded P to lsum by v_dot2 against `ones` (a pair of ones in the
-// compute dtype): 8 ops instead of 15 fp32 adds. DH 80: the sum rides the P.V
-// MFMAs (V's padding dims 80-87 are ones: O^T rows 80-87 = sum_k P).
+// (pf[s2]: accumulator regs 8 s2 .. 8 s2 + 7) and, for DH 64, adds the fp32 row
+// sum to lsum. DH 80: the sum rides the P.V MFMAs (V's padding dims 80-87 are
+// ones: O^T rows 80-87 = sum_k P).
 template <typename T, int DH>
 MICLIP_DEV void softmax_tile(f32x16& sacc, float c2, float& m, float& lsum,
-                             f32x16 (&o)[HeadGeom<DH>::NDT], i16x8 (&pf)[2], uint32_t ones) {
+                             f32x16 (&o)[HeadGeom<DH>::NDT], i16x8 (&pf)[2]) {
   // a v_max3 tree: 8 ops for 16 values
   const float t0 = fmaxf(fmaxf(sacc[0], sacc[1]), sacc[2]);
   const float t1 = fmaxf(fmaxf(sacc[3], sacc[4]), sacc[5]);
@@ -149,27 +148,25 @@ MICLIP_DEV void softmax_tile(f32x16& sacc, float c2, float& m, float& lsum,
   // P operand anyway. Scalar f32 ops on purpose (this file builds with
   // -fno-slp-vectorize): beside MFMAs a v_pk_fma_f32 issues slower than the two
   // scalar ops it replaces (MI355X_MICROARCH.md, per-instruction constants).
+  // (four partial sums break the add dependency chain; they start at the first
+  // four values: 0 + v == v for the non-negative exponentials)
+  float ps[4];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) sacc[r] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[r], c2, -m));
+  for (int r = 0; r < 16; ++r) {
+    const float v = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[r], c2, -m));
+    sacc[r] = v;
+    if constexpr (DH != 80) {
+      if (r < 4)
+        ps[r] = v;
+      else
+        ps[r & 3] += v;
+    }
+  }
+  if constexpr (DH != 80) lsum += (ps[0] + ps[2]) + (ps[1] + ps[3]);
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
     for (int j = 0; j < 8; ++j) pf[s2][j] = to_bits<T>(sacc[8 * s2 + j]);
-  if constexpr (DH != 80) {
-    const u32x4 a = __builtin_bit_cast(u32x4, pf[0]), b = __builtin_bit_cast(u32x4, pf[1]);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) lsum = dot2acc<T>(a[e], ones, lsum);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) lsum = dot2acc<T>(b[e], ones, lsum);
-  }
-}
-
-// a pair of ones in the compute dtype, in a VGPR (softmax_tile's row sums)
-template <typename T>
-MICLIP_DEV uint32_t ones_pair() {
-  uint32_t ones = (uint32_t)(to_bits<T>(1.0f) & 0xffff) * 0x10001u;
-  asm("" : "+v"(ones));
-  return ones;
 }
 
 // One wave: 32 queries [32*chunk, +32) of one (image, head) against all keys
@@ -181,7 +178,7 @@ MICLIP_DEV uint32_t ones_pair() {
 // first / last: a key range processed in several calls starts the online
 // softmax state in the first call and reduces lsum across the lane halves in
 // the last one (both true: one call over the range).
-template <typename T, bool CAUSAL, int DH, bool PIPE = true>
+template <typename T, bool CAUSAL, int DH, bool PIPE = true, bool OPQ = false>
 MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
                              const i16x8 (&qf)[HeadGeom<DH>::NKS], int chunk, int N, int Npad,
                              float c2, int lane, f32x16 (&o)[HeadGeom<DH>::NDT], float& lsum,
@@ -226,9 +223,14 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
   // 32-bit LDS addresses (address space 3) from an opaque wave-uniform base: the
   // images' base is otherwise re-added to every per-lane offset at every read
   // (the dynamic-LDS symbol is a relocation hipcc does not fold)
+  // 32-bit LDS addresses (address space 3). OPQ: from an opaque wave-uniform base
+  // -- the dynamic-LDS symbol is a relocation hipcc otherwise re-adds to every
+  // per-lane offset at every read (6 VALU per key tile); it costs registers, so
+  // only the x8 kernel (122 of its 128 VGPRs) takes it (the 16-wave
+  // attention_kernel<64> spilled with it)
   unsigned kb = (unsigned)(uintptr_t)(const LDS_AS char*)kimg;
   unsigned vb = (unsigned)(uintptr_t)(const LDS_AS char*)vimg;
-  asm("" : "+s"(kb), "+s"(vb));
+  if constexpr (OPQ) asm("" : "+s"(kb), "+s"(vb));
   const LDS_AS char* kl = (const LDS_AS char*)(uintptr_t)kb;
   const LDS_AS char* vl = (const LDS_AS char*)(uintptr_t)vb;
   auto qk = [&](int kt, f32x16& sacc) {
@@ -243,7 +245,6 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
     }
     __builtin_amdgcn_s_setprio(0);
   };
-  const uint32_t ones = ones_pair<T>();
   auto softmax_pv = [&](int kt, f32x16& sacc) {
     const LDS_AS char* vtile = vl + kt * G::TILEB;
     // ---- mask (only tiles that need it), then the online softmax ----
@@ -257,7 +258,7 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
       }
     }
     i16x8 pf[2];
-    softmax_tile<T, DH>(sacc, c2, m, lsum, o, pf, ones);
+    softmax_tile<T, DH>(sacc, c2, m, lsum, o, pf);
     // ---- O^T[d][q] += V^T . P^T ----
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -300,86 +301,6 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
     if (last) lsum = o[2][8];
   } else {
     if (last) lsum = xor32_sum(lsum);
-  }
-}
-
-// Two 32-query chunks (qa, qb) of one (image, head), head dim 64, against the 8
-// full key tiles [0, 256), interleaved tile by tile in one wave: each tile's K
-// and V fragments are read from LDS once for both chunks (half the LDS reads per
-// MFMA of attend_chunk), V's before the S MFMAs so they land under them, and
-// the two chunks' S -> softmax -> P.V chains are independent, so one chain's
-// softmax VALU issues while the other's MFMAs run (two waves' worth of latency
-// hiding in one wave). Per chunk the arithmetic is attend_chunk's (first = true,
-// last = false: lsum is reduced across the lane halves by the caller).
-template <typename T>
-MICLIP_DEV void attend_pair(const char* kimg, const char* vimg, const i16x8 (&qa)[4],
-                            const i16x8 (&qb)[4], float c2, int lane, f32x16 (&oa)[2],
-                            f32x16 (&ob)[2], float& la, float& lb, float& ma, float& mb) {
-  using G = HeadGeom<64>;
-  const int l32 = lane & 31, hh = lane >> 5;
-  const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
-  ma = mb = -1e30f;
-  la = lb = 0.f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r)
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) oa[dt][r] = ob[dt][r] = 0.f;
-  int koff[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) koff[s] = l32 * G::ROWB + (G::kswz(2 * s + hh, l32) << 4);
-  int voff[2];
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt) {
-    const int ch = 4 * dt + 2 * (g & 1) + (tp >> 1);
-    voff[dt] = (4 * (g >> 1) + tq) * G::ROWB + (G::vswz(ch, 4 * (g >> 1) + tq) << 4) + 8 * (tp & 1);
-  }
-  unsigned kb = (unsigned)(uintptr_t)(const LDS_AS char*)kimg;
-  unsigned vb = (unsigned)(uintptr_t)(const LDS_AS char*)vimg;
-  asm("" : "+s"(kb), "+s"(vb));
-  const LDS_AS char* kl = (const LDS_AS char*)(uintptr_t)kb;
-  const LDS_AS char* vl = (const LDS_AS char*)(uintptr_t)vb;
-  const uint32_t ones = ones_pair<T>();
-  for (int kt = 0; kt < 8; ++kt) {
-    const LDS_AS char* ktile = kl + kt * G::TILEB;
-    const LDS_AS char* vtile = vl + kt * G::TILEB;
-    i16x8 kf[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) kf[s] = *(const LDS_AS i16x8*)(ktile + koff[s]);
-    i16x8 vf[2][2];   // [k-step s2][dim tile dt]
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        const LDS_AS char* a0 = vtile + voff[dt] + 16 * G::ROWB * s2;
-        const i16x4 lo = ds_read_tr16_b64(a0);
-        const i16x4 hi = ds_read_tr16_b64(a0 + 8 * G::ROWB);
-        vf[s2][dt] = (i16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-    f32x16 sa, sb;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sa[r] = sb[r] = 0.f;
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      sa = Mfma<T>::m32(kf[s], qa[s], sa);
-      sb = Mfma<T>::m32(kf[s], qb[s], sb);
-    }
-    __builtin_amdgcn_s_setprio(0);
-    i16x8 pa[2], pb[2];
-    softmax_tile<T, 64>(sa, c2, ma, la, oa, pa, ones);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) oa[dt] = Mfma<T>::m32(vf[s2][dt], pa[s2], oa[dt]);
-    __builtin_amdgcn_s_setprio(0);
-    softmax_tile<T, 64>(sb, c2, mb, lb, ob, pb, ones);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) ob[dt] = Mfma<T>::m32(vf[s2][dt], pb[s2], ob[dt]);
-    __builtin_amdgcn_s_setprio(0);
   }
 }
 
@@ -426,8 +347,8 @@ MICLIP_DEV void attend_extra_keys(const char* kimg, const char* vimg, const i16x
       }
     }
     const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(score, c2, -m));
+    if (hh == 0) lsum += p;
     const float p16 = to_f<T>(to_t<T>(p));
-    if (hh == 0) lsum += p16;   // the row sum of the P used, as attend_chunk's
     const char* vr = vimg + (k - row0) * 128;
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
@@ -838,8 +759,7 @@ template <typename T>
 __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restrict__ qkv,
                                                              T* __restrict__ out, int B, int N,
                                                              int H, int Npad, int hpw,
-                                                             float qk_scale, int prio,
-                                                             int hm = 0) {
+                                                             float qk_scale, int prio) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int img_bytes = Npad * 128;
   char* kimg = smem;
@@ -851,10 +771,7 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
   const int nextra = N - 256;                // keys past the 8 full tiles (attend_extra_keys)
   (void)ntiles;
   float* part = (float*)(smem + 2 * img_bytes);   // [8 waves][nvalid][66]
-  // hm (head-major input, a layout probe): qkv [B][H][3][N][64] -- each head's Q,
-  // K and V rows contiguous -- instead of the projection's token-major [B N][3 D]
-  const int D = H * 64, ld = hm ? 64 : 3 * D;
-  const int koff = hm ? N * 64 : D, voff = hm ? 2 * N * 64 : 2 * D;
+  const int D = H * 64, ld = 3 * D;
   const float c2 = qk_scale * kLog2e;
   const int bh0 = blockIdx.x * hpw;
   const int nh = (B * H - bh0) < hpw ? (B * H - bh0) : hpw;
@@ -863,7 +780,6 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
   const int pieces = (N + 7) / 8;
   const int prow = lane >> 3, pch = lane & 7;
   auto head_base = [&](int bh) {
-    if (hm) return qkv + (size_t)bh * 3 * N * 64;
     const int b = bh / H, h = bh - b * H;
     return qkv + (size_t)b * N * ld + h * 64;
   };
@@ -879,7 +795,7 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
       const int row = piece * 8 + prow;
       const int r = row < N ? row : N - 1;   // pad rows: finite data, masked keys
       const int lch = isv ? (pch ^ ((row & 3) << 1)) : (pch ^ ((row >> 1) & 7));
-      glds16_hidden(base + (size_t)r * ld + (isv ? voff : koff) + lch * 8,
+      glds16_hidden(base + (size_t)r * ld + (isv ? 2 * D : D) + lch * 8,
                     (isv ? vimg : kimg) + piece * 1024);
     }
     MICLIP_STAMP(6);   // DMA issue
@@ -893,8 +809,8 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
     {
       f32x16 o[2];
       float lsum, m;
-      attend_chunk<T, false, 64, false>(kimg, vimg, qf, wave, N, Npad, c2, lane, o, lsum, m, 0, 8,
-                                        prio, true, false);
+      attend_chunk<T, false, 64, false, true>(kimg, vimg, qf, wave, N, Npad, c2, lane, o, lsum, m,
+                                              0, 8, prio, true, false);
       attend_extra_keys<T>(kimg, vimg, qf, o, lsum, m, 256, nextra, c2, lane);
       lsum = xor32_sum(lsum);
       MICLIP_STAMP(1);   // the wave's full query chunk
@@ -906,8 +822,8 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
       f32x16 o[2];
       float lsum, m;
       // key tile `wave` of the 8 full ones (the keys past them: in the merge)
-      attend_chunk<T, false, 64, false>(kimg, vimg, qf, 8, N, Npad, c2, lane, o, lsum, m, wave,
-                                        wave + 1, prio);
+      attend_chunk<T, false, 64, false, true>(kimg, vimg, qf, 8, N, Npad, c2, lane, o, lsum, m,
+                                              wave, wave + 1, prio);
       // lane (l32, hh) holds O^T rows d = (r&3) + 8*(r>>2) + 4*hh (+32 in o[1]) of query l32
       const int l32 = lane & 31, hh = lane >> 5;
       if (l32 < nvalid) {
@@ -940,9 +856,8 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
         const float mn = fmaxf(me, sc), al = __builtin_amdgcn_exp2f(me - mn);
         const float p = __builtin_amdgcn_exp2f(sc - mn);
         const float vd = to_f<T>(*(const T*)(vimg + k * 128 + ((ch ^ ((k & 3) << 1)) << 4) + (lane & 7) * 2));
-        const float pr = to_f<T>(to_t<T>(p));   // the P used, rounded
-        le = le * al + pr;
-        oe = oe * al + pr * vd;
+        le = le * al + p;
+        oe = oe * al + to_f<T>(to_t<T>(p)) * vd;
         me = mn;
       }
     }
@@ -974,467 +889,6 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
   MICLIP_STAMP_END(blockIdx.x * 8 + wave);
 }
 
-
-// ---------------------------------------------------------------------------
-// Phase-locked pair (variant 20, N in 256..259): ONE workgroup of 16 waves per
-// CU holds two groups of 8 waves, each doing the x8 kernel's per-head work
-// (wave w: query chunk w over the 8 full key tiles + the extra keys, key tile w
-// of the ragged chunk, the ragged query's extra-keys partial) with its own K/V
-// image and ragged partials in LDS. Workgroup barriers cut time into phases: in
-// each one a group computes a head while the other fetches its next head (K/V
-// by LDS-DMA, its Q fragments into registers) and merges the ragged query of
-// the head it computed before. The groups swap roles every phase (group 0
-// fetches on even phases, group 1 on odd ones, one head behind), so the CU's
-// memory stream and its compute stay busy together -- two independent x8
-// workgroups on a CU drift into fetching, and computing, at the same time.
-// Every wave runs the same 2 hpg + 1 phases (one barrier each).
-// ---------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(1024, 1) void attention_x16_kernel(const T* __restrict__ qkv,
-                                                               T* __restrict__ out, int B, int N,
-                                                               int H, int Npad, int hpg,
-                                                               int img_bytes, int grp_bytes,
-                                                               float qk_scale, int prio) {
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int grp = wave >> 3, gw = wave & 7;
-  char* kimg = smem + grp * grp_bytes;
-  char* vimg = kimg + img_bytes;
-  float* part = (float*)(vimg + img_bytes);      // [8 waves][nvalid][66]
-  const int nvalid = N - 256;                    // queries of the ragged chunk 8
-  const int nextra = N - 256;                    // keys past the 8 full tiles
-  const int D = H * 64, ld = 3 * D;
-  const float c2 = qk_scale * kLog2e;
-  const int bh0 = (blockIdx.x * 2 + grp) * hpg;
-  const int nh = B * H - bh0 < 0 ? 0 : (B * H - bh0 < hpg ? B * H - bh0 : hpg);
-  const int pieces = (N + 7) / 8;
-  const int prow = lane >> 3, pch = lane & 7;
-  auto head_base = [&](int bh) {
-    const int b = bh / H, h = bh - b * H;
-    return qkv + (size_t)b * N * ld + h * 64;
-  };
-  auto out_base = [&](int bh) {
-    const int b = bh / H, h = bh - b * H;
-    return out + (size_t)b * N * D + h * 64;
-  };
-  i16x8 qf[4];
-  // the ragged query gw's partial over the extra keys (computed while the head's
-  // K / V are resident, merged in the group's next fetch phase)
-  float me = -1e30f, le = 0.f, oe = 0.f;
-  int prev = -1;   // head whose ragged query awaits its merge
-  auto merge = [&](int j) {
-    if (gw < nvalid) {
-      const float* pc = part + (size_t)gw * 66;
-      float mx = me;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) mx = fmaxf(mx, pc[(size_t)i * nvalid * 66 + 64]);
-      const float we = __builtin_amdgcn_exp2f(me - mx);
-      float l = we * le, acc = we * oe;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float* pi = pc + (size_t)i * nvalid * 66;
-        const float w = __builtin_amdgcn_exp2f(pi[64] - mx);
-        l += w * pi[65];
-        acc += w * pi[lane];
-      }
-      out_base(bh0 + j)[(size_t)(256 + gw) * D + lane] = to_t<T>(acc / l);
-    }
-  };
-  for (int ph = 0; ph <= 2 * hpg; ++ph) {
-    const bool fetch = (ph & 1) == grp;
-    const int j = grp == 0 ? (fetch ? ph / 2 : (ph - 1) / 2) : (fetch ? (ph - 1) / 2 : ph / 2 - 1);
-    if (fetch) {
-      if (j < nh) {
-        // this group's K / V images are free: its previous head was computed in
-        // the phase before the last barrier
-        const T* base = head_base(bh0 + j);
-        for (int pc = gw; pc < 2 * pieces; pc += 8) {
-          const bool isv = pc >= pieces;
-          const int piece = isv ? pc - pieces : pc;
-          const int row = piece * 8 + prow;
-          const int r = row < N ? row : N - 1;
-          const int lch = isv ? (pch ^ ((row & 3) << 1)) : (pch ^ ((row >> 1) & 7));
-          glds16_hidden(base + (size_t)r * ld + (isv ? 2 * D : D) + lch * 8,
-                        (isv ? vimg : kimg) + piece * 1024);
-        }
-        load_q<T, 64>(qf, base, ld, gw, N, lane);
-      }
-      if (prev >= 0) merge(prev);   // reads the partials only, not the images
-      prev = -1;
-      if (j < nh)
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
-    } else if (j >= 0 && j < nh) {
-      const T* base = head_base(bh0 + j);
-      T* obase = out_base(bh0 + j);
-      {
-        f32x16 o[2];
-        float lsum, m;
-        attend_chunk<T, false, 64, false>(kimg, vimg, qf, gw, N, Npad, c2, lane, o, lsum, m, 0, 8,
-                                          prio, true, false);
-        attend_extra_keys<T>(kimg, vimg, qf, o, lsum, m, 256, nextra, c2, lane);
-        lsum = xor32_sum(lsum);
-        attend_store<T, 64>(o, lsum, gw, N, obase, D, lane);
-      }
-      if (nvalid > 0) {
-        load_q<T, 64>(qf, base, ld, 8, N, lane);
-        f32x16 o[2];
-        float lsum, m;
-        attend_chunk<T, false, 64, false>(kimg, vimg, qf, 8, N, Npad, c2, lane, o, lsum, m, gw,
-                                          gw + 1, prio);
-        const int l32 = lane & 31, hh = lane >> 5;
-        if (l32 < nvalid) {
-          float* pw = part + ((size_t)gw * nvalid + l32) * 66;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int d = (r & 3) + 8 * (r >> 2) + 4 * hh;
-            pw[d] = o[0][r];
-            pw[32 + d] = o[1][r];
-          }
-          if (hh == 0) {
-            pw[64] = m;
-            pw[65] = lsum;
-          }
-        }
-        me = -1e30f;
-        le = 0.f;
-        oe = 0.f;
-        if (gw < nvalid) {
-          const float qd = to_f<T>(base[(size_t)(256 + gw) * ld + lane]);
-          const int ch = lane >> 3;
-          for (int k = 256; k < N; ++k) {
-            const float kd = to_f<T>(*(const T*)(kimg + k * 128 + ((ch ^ ((k >> 1) & 7)) << 4) + (lane & 7) * 2));
-            const float sc = wave_sum(qd * kd) * c2;
-            const float mn = fmaxf(me, sc), al = __builtin_amdgcn_exp2f(me - mn);
-            const float p = __builtin_amdgcn_exp2f(sc - mn);
-            const float vd = to_f<T>(*(const T*)(vimg + k * 128 + ((ch ^ ((k & 3) << 1)) << 4) + (lane & 7) * 2));
-            const float pr = to_f<T>(to_t<T>(p));   // the P used, rounded
-            le = le * al + pr;
-            oe = oe * al + pr * vd;
-            me = mn;
-          }
-        }
-        prev = j;
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-  if (prev >= 0) merge(prev);
-}
-
-// ---------------------------------------------------------------------------
-// Loader + consumer waves (variant 21, N in 256..259): ONE workgroup of 12 waves
-// per CU, two K/V buffers. Waves 8-11 (loaders) only stream the next head's K/V
-// into the other buffer by LDS-DMA and wait for it; waves 0-7 (consumers) never
-// issue a DMA: wave w computes query chunk w of the current head over the 8
-// full key tiles (two score tiles in flight, attend_chunk PIPE) + the extra keys,
-// key tile w of the ragged chunk (flash-decoding partial to LDS) and, w <
-// N - 256, the ragged query w's extra-keys partial; its next head's Q fragments
-// are prefetched into registers during the head. One workgroup barrier per head;
-// the ragged query of head j is merged (fixed order, as the x8 kernel) by waves
-// w < N - 256 after the barrier that ends it, from partials double-buffered by
-// head parity. 3 waves per SIMD: a 170-VGPR budget.
-// ---------------------------------------------------------------------------
-template <typename T, bool PIPE>
-__global__ __launch_bounds__(768, 1) void attention_lc_kernel(const T* __restrict__ qkv,
-                                                             T* __restrict__ out, int B, int N,
-                                                             int H, int Npad, int hpw,
-                                                             int img_bytes, float qk_scale,
-                                                             int prio) {
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool loader = wave >= 8;
-  const int nvalid = N - 256, nextra = N - 256;
-  float* part = (float*)(smem + 4 * img_bytes);   // [2][8 waves][nvalid][66]
-  const int D = H * 64, ld = 3 * D;
-  const float c2 = qk_scale * kLog2e;
-  const int bh0 = blockIdx.x * hpw;
-  const int nh = B * H - bh0 < hpw ? B * H - bh0 : hpw;
-  const int pieces = (N + 7) / 8;
-  const int prow = lane >> 3, pch = lane & 7;
-  auto head_base = [&](int bh) {
-    const int b = bh / H, h = bh - b * H;
-    return qkv + (size_t)b * N * ld + h * 64;
-  };
-  auto out_base = [&](int bh) {
-    const int b = bh / H, h = bh - b * H;
-    return out + (size_t)b * N * D + h * 64;
-  };
-  auto stage = [&](int bh, int buf) {   // loaders: 2 x pieces 1-KiB DMAs over 4 waves
-    const T* base = head_base(bh);
-    char* kimg = smem + buf * 2 * img_bytes;
-    char* vimg = kimg + img_bytes;
-    for (int pc = wave - 8; pc < 2 * pieces; pc += 4) {
-      const bool isv = pc >= pieces;
-      const int piece = isv ? pc - pieces : pc;
-      const int row = piece * 8 + prow;
-      const int r = row < N ? row : N - 1;
-      const int lch = isv ? (pch ^ ((row & 3) << 1)) : (pch ^ ((row >> 1) & 7));
-      glds16_hidden(base + (size_t)r * ld + (isv ? 2 * D : D) + lch * 8,
-                    (isv ? vimg : kimg) + piece * 1024);
-    }
-  };
-  float me = -1e30f, le = 0.f, oe = 0.f;   // ragged query `wave`'s extra-keys partial
-  auto merge = [&](int j) {                // head j's ragged query `wave`
-    const float* pc = part + ((size_t)((j & 1) * 8) * nvalid + wave) * 66;
-    float mx = me;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) mx = fmaxf(mx, pc[(size_t)i * nvalid * 66 + 64]);
-    const float we = __builtin_amdgcn_exp2f(me - mx);
-    float l = we * le, acc = we * oe;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float* pi = pc + (size_t)i * nvalid * 66;
-      const float w = __builtin_amdgcn_exp2f(pi[64] - mx);
-      l += w * pi[65];
-      acc += w * pi[lane];
-    }
-    out_base(bh0 + j)[(size_t)(256 + wave) * D + lane] = to_t<T>(acc / l);
-  };
-  i16x8 qf[4], qn[4], qx[4];
-  if (nh > 0) {
-    if (loader) {
-      stage(bh0, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      load_q<T, 64>(qf, head_base(bh0), ld, wave, N, lane);
-      asm volatile("s_waitcnt vmcnt(0)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
-    }
-  }
-  __builtin_amdgcn_s_barrier();
-  for (int j = 0; j < nh; ++j) {
-    if (loader) {
-      if (j + 1 < nh) {
-        stage(bh0 + j + 1, (j + 1) & 1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    } else {
-      if (j > 0 && wave < nvalid) merge(j - 1);
-      const T* base = head_base(bh0 + j);
-      if (j + 1 < nh) load_q<T, 64>(qn, head_base(bh0 + j + 1), ld, wave, N, lane);
-      if (nvalid > 0) load_q<T, 64>(qx, base, ld, 8, N, lane);
-      const char* kimg = smem + (j & 1) * 2 * img_bytes;
-      const char* vimg = kimg + img_bytes;
-      {
-        f32x16 o[2];
-        float lsum, m;
-        attend_chunk<T, false, 64, PIPE>(kimg, vimg, qf, wave, N, Npad, c2, lane, o, lsum, m, 0, 8,
-                                         prio, true, false);
-        attend_extra_keys<T>(kimg, vimg, qf, o, lsum, m, 256, nextra, c2, lane);
-        lsum = xor32_sum(lsum);
-        attend_store<T, 64>(o, lsum, wave, N, out_base(bh0 + j), D, lane);
-      }
-      if (nvalid > 0) {
-        f32x16 o[2];
-        float lsum, m;
-        attend_chunk<T, false, 64, false>(kimg, vimg, qx, 8, N, Npad, c2, lane, o, lsum, m, wave,
-                                          wave + 1, prio);
-        const int l32 = lane & 31, hh = lane >> 5;
-        if (l32 < nvalid) {
-          float* pw = part + ((size_t)((j & 1) * 8 + wave) * nvalid + l32) * 66;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int d = (r & 3) + 8 * (r >> 2) + 4 * hh;
-            pw[d] = o[0][r];
-            pw[32 + d] = o[1][r];
-          }
-          if (hh == 0) {
-            pw[64] = m;
-            pw[65] = lsum;
-          }
-        }
-        me = -1e30f;
-        le = 0.f;
-        oe = 0.f;
-        if (wave < nvalid) {
-          const float qd = to_f<T>(base[(size_t)(256 + wave) * ld + lane]);
-          const int ch = lane >> 3;
-          for (int k = 256; k < N; ++k) {
-            const float kd = to_f<T>(*(const T*)(kimg + k * 128 + ((ch ^ ((k >> 1) & 7)) << 4) + (lane & 7) * 2));
-            const float sc = wave_sum(qd * kd) * c2;
-            const float mn = fmaxf(me, sc), al = __builtin_amdgcn_exp2f(me - mn);
-            const float p = __builtin_amdgcn_exp2f(sc - mn);
-            const float vd = to_f<T>(*(const T*)(vimg + k * 128 + ((ch ^ ((k & 3) << 1)) << 4) + (lane & 7) * 2));
-            const float pr = to_f<T>(to_t<T>(p));   // the P used, rounded
-            le = le * al + pr;
-            oe = oe * al + pr * vd;
-            me = mn;
-          }
-        }
-      }
-      if (j + 1 < nh) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) qf[q] = qn[q];
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-  if (!loader && nh > 0 && wave < nvalid) merge(nh - 1);
-}
-
-// ---------------------------------------------------------------------------
-// Chunk pairs + loader waves (variant 23, N in 256..259): ONE workgroup of 8
-// waves per CU (2 per SIMD: a 256-VGPR budget), two K/V buffers.
-//   * waves 0-3 (consumers): wave w computes query chunks w and w + 4 of the
-//     current head together (attend_pair: K / V fragments read once for both,
-//     two independent chains per wave) plus each chunk's extra keys, and
-//     prefetches its next head's Q fragments into registers;
-//   * waves 4-7 (loaders): stream the next head's K/V into the other buffer by
-//     LDS-DMA, and compute the ragged chunk (the N - 256 queries past the 8 full
-//     chunks) of the current head: loader l takes key tiles 2l, 2l + 1 as a
-//     flash-decoding partial (LDS, double-buffered by head parity), loader l <
-//     N - 256 also ragged query l's extra keys; after the barrier that ends a
-//     head, loader l < N - 256 merges ragged query l (fixed order).
-// One workgroup barrier per head. Same arithmetic per element as the x8 kernel
-// except the ragged query's merge order (4 two-tile partials instead of 8).
-// ---------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(512, 1) void attention_pair_kernel(const T* __restrict__ qkv,
-                                                               T* __restrict__ out, int B, int N,
-                                                               int H, int Npad, int hpw,
-                                                               int img_bytes, float qk_scale) {
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool loader = wave >= 4;
-  const int lw = wave - 4;                        // loader index
-  const int nvalid = N - 256, nextra = N - 256;
-  float* part = (float*)(smem + 4 * img_bytes);   // [2][4 loaders][nvalid][66]
-  const int D = H * 64, ld = 3 * D;
-  const float c2 = qk_scale * kLog2e;
-  const int bh0 = blockIdx.x * hpw;
-  const int nh = B * H - bh0 < hpw ? B * H - bh0 : hpw;
-  const int pieces = (N + 7) / 8;
-  const int prow = lane >> 3, pch = lane & 7;
-  auto head_base = [&](int bh) {
-    const int b = bh / H, h = bh - b * H;
-    return qkv + (size_t)b * N * ld + h * 64;
-  };
-  auto out_base = [&](int bh) {
-    const int b = bh / H, h = bh - b * H;
-    return out + (size_t)b * N * D + h * 64;
-  };
-  auto stage = [&](int bh, int buf) {   // loaders: 2 x pieces 1-KiB DMAs over 4 waves
-    const T* base = head_base(bh);
-    char* kimg = smem + buf * 2 * img_bytes;
-    char* vimg = kimg + img_bytes;
-    for (int pc = lw; pc < 2 * pieces; pc += 4) {
-      const bool isv = pc >= pieces;
-      const int piece = isv ? pc - pieces : pc;
-      const int row = piece * 8 + prow;
-      const int r = row < N ? row : N - 1;
-      const int lch = isv ? (pch ^ ((row & 3) << 1)) : (pch ^ ((row >> 1) & 7));
-      glds16_hidden(base + (size_t)r * ld + (isv ? 2 * D : D) + lch * 8,
-                    (isv ? vimg : kimg) + piece * 1024);
-    }
-  };
-  float me = -1e30f, le = 0.f, oe = 0.f;   // ragged query lw's extra-keys partial
-  auto merge = [&](int j) {                // head j's ragged query lw
-    const float* pc = part + ((size_t)((j & 1) * 4) * nvalid + lw) * 66;
-    float mx = me;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) mx = fmaxf(mx, pc[(size_t)i * nvalid * 66 + 64]);
-    const float we = __builtin_amdgcn_exp2f(me - mx);
-    float l = we * le, acc = we * oe;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float* pi = pc + (size_t)i * nvalid * 66;
-      const float w = __builtin_amdgcn_exp2f(pi[64] - mx);
-      l += w * pi[65];
-      acc += w * pi[lane];
-    }
-    out_base(bh0 + j)[(size_t)(256 + lw) * D + lane] = to_t<T>(acc / l);
-  };
-  i16x8 qa[4], qb[4];
-  if (nh > 0) {
-    if (loader) {
-      stage(bh0, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      load_q<T, 64>(qa, head_base(bh0), ld, wave, N, lane);
-      load_q<T, 64>(qb, head_base(bh0), ld, wave + 4, N, lane);
-      asm volatile("s_waitcnt vmcnt(0)"
-                   : "+v"(qa[0]), "+v"(qa[1]), "+v"(qa[2]), "+v"(qa[3]), "+v"(qb[0]), "+v"(qb[1]),
-                     "+v"(qb[2]), "+v"(qb[3])::"memory");
-    }
-  }
-  __builtin_amdgcn_s_barrier();
-  for (int j = 0; j < nh; ++j) {
-    const T* base = head_base(bh0 + j);
-    const char* kimg = smem + (j & 1) * 2 * img_bytes;
-    const char* vimg = kimg + img_bytes;
-    if (loader) {
-      if (j + 1 < nh) stage(bh0 + j + 1, (j + 1) & 1);
-      // the previous head's ragged query first: me / le / oe are about to be
-      // overwritten by this head's
-      if (j > 0 && lw < nvalid) merge(j - 1);
-      if (nvalid > 0) {
-        i16x8 qx[4];
-        load_q<T, 64>(qx, base, ld, 8, N, lane);
-        f32x16 o[2];
-        float lsum, m;
-        attend_chunk<T, false, 64, false>(kimg, vimg, qx, 8, N, Npad, c2, lane, o, lsum, m, 2 * lw,
-                                          2 * lw + 2, 1);
-        const int l32 = lane & 31, hh = lane >> 5;
-        if (l32 < nvalid) {
-          float* pw = part + ((size_t)((j & 1) * 4 + lw) * nvalid + l32) * 66;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int d = (r & 3) + 8 * (r >> 2) + 4 * hh;
-            pw[d] = o[0][r];
-            pw[32 + d] = o[1][r];
-          }
-          if (hh == 0) {
-            pw[64] = m;
-            pw[65] = lsum;
-          }
-        }
-        me = -1e30f;
-        le = 0.f;
-        oe = 0.f;
-        if (lw < nvalid) {
-          const float qd = to_f<T>(base[(size_t)(256 + lw) * ld + lane]);
-          const int ch = lane >> 3;
-          for (int k = 256; k < N; ++k) {
-            const float kd = to_f<T>(*(const T*)(kimg + k * 128 + ((ch ^ ((k >> 1) & 7)) << 4) + (lane & 7) * 2));
-            const float sc = wave_sum(qd * kd) * c2;
-            const float mn = fmaxf(me, sc), al = __builtin_amdgcn_exp2f(me - mn);
-            const float p = __builtin_amdgcn_exp2f(sc - mn);
-            const float vd = to_f<T>(*(const T*)(vimg + k * 128 + ((ch ^ ((k & 3) << 1)) << 4) + (lane & 7) * 2));
-            const float pr = to_f<T>(to_t<T>(p));   // the P used, rounded
-            le = le * al + pr;
-            oe = oe * al + pr * vd;
-            me = mn;
-          }
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next head's K / V landed
-    } else {
-      f32x16 oa[2], ob[2];
-      float la, lb, ma, mb;
-      attend_pair<T>(kimg, vimg, qa, qb, c2, lane, oa, ob, la, lb, ma, mb);
-      attend_extra_keys<T>(kimg, vimg, qa, oa, la, ma, 256, nextra, c2, lane);
-      attend_extra_keys<T>(kimg, vimg, qb, ob, lb, mb, 256, nextra, c2, lane);
-      la = xor32_sum(la);
-      lb = xor32_sum(lb);
-      attend_store<T, 64>(oa, la, wave, N, out_base(bh0 + j), D, lane);
-      attend_store<T, 64>(ob, lb, wave + 4, N, out_base(bh0 + j), D, lane);
-      if (j + 1 < nh) {   // the next head's Q (its latency overlaps the barrier wait)
-        load_q<T, 64>(qa, head_base(bh0 + j + 1), ld, wave, N, lane);
-        load_q<T, 64>(qb, head_base(bh0 + j + 1), ld, wave + 4, N, lane);
-        asm volatile("s_waitcnt vmcnt(0)"
-                     : "+v"(qa[0]), "+v"(qa[1]), "+v"(qa[2]), "+v"(qa[3]), "+v"(qb[0]), "+v"(qb[1]),
-                       "+v"(qb[2]), "+v"(qb[3])::"memory");
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-  if (loader && nh > 0 && lw < nvalid) merge(nh - 1);
-}
 
 // ---------------------------------------------------------------------------
 // One query per (image, head): token row 0 (CLS) only. The vision tower's last
@@ -1620,102 +1074,7 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, 
   // must stay under 80 KiB of LDS, i.e. N - 256 <= 3)
   const size_t lds_x8 = lds + (size_t)8 * (N > 256 ? N - 256 : 0) * 66 * 4;
   if (variant == 9) return hipErrorInvalidValue;   // removed (measured level)
-  const int img16 = ((N + 7) / 8) * 1024, grp16 = 2 * img16 + 8 * (N > 256 ? N - 256 : 0) * 66 * 4;
-  if (variant == 23) {
-    // chunk pairs + loader waves, one 8-wave workgroup per CU (attention_pair_kernel)
-    if (CAUSAL || N < 256 || N > 259) return hipErrorInvalidValue;
-    const size_t lds_p = (size_t)4 * img16 + (size_t)2 * 4 * (N - 256) * 66 * 4;
-    if (lds_p > 160 * 1024) return hipErrorInvalidValue;
-    static bool p_attr = false;
-    if (!p_attr) {
-      const hipError_t e = hipFuncSetAttribute((const void*)attention_pair_kernel<T>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               160 * 1024);
-      if (e != hipSuccess) return e;
-      p_attr = true;
-    }
-    static int ncu_p = [] {
-      int d = 0, n = 0;
-      if (hipGetDevice(&d) != hipSuccess ||
-          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
-        n = 256;
-      return n;
-    }();
-    const int heads = B * H;
-    int hpw = (heads + ncu_p - 1) / ncu_p;
-    hpw = hpw < 1 ? 1 : hpw;
-    const int grid = (heads + hpw - 1) / hpw;
-    hipLaunchKernelGGL((attention_pair_kernel<T>), dim3(grid), dim3(512), lds_p, s,
-                       (const T*)qkv, (T*)out, B, N, H, Npad, hpw, img16, 0.125f);
-    return hipGetLastError();
-  }
-  if (variant == 21 || variant == 22) {
-    // loader + consumer waves, one 12-wave workgroup per CU (attention_lc_kernel;
-    // 21: two score tiles in flight, 22: one)
-    if (CAUSAL || N < 256 || N > 259) return hipErrorInvalidValue;
-    const size_t lds_lc = (size_t)4 * img16 + (size_t)2 * 8 * (N - 256) * 66 * 4;
-    if (lds_lc > 160 * 1024) return hipErrorInvalidValue;
-    static bool lc_attr = false;
-    if (!lc_attr) {
-      for (const void* k : {(const void*)attention_lc_kernel<T, true>,
-                            (const void*)attention_lc_kernel<T, false>}) {
-        const hipError_t e =
-            hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return e;
-      }
-      lc_attr = true;
-    }
-    static int ncu_lc = [] {
-      int d = 0, n = 0;
-      if (hipGetDevice(&d) != hipSuccess ||
-          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
-        n = 256;
-      return n;
-    }();
-    const int heads = B * H;
-    int hpw = (heads + ncu_lc - 1) / ncu_lc;
-    hpw = hpw < 1 ? 1 : hpw;
-    const int grid = (heads + hpw - 1) / hpw;
-    if (variant == 21)
-      hipLaunchKernelGGL((attention_lc_kernel<T, true>), dim3(grid), dim3(768), lds_lc, s,
-                         (const T*)qkv, (T*)out, B, N, H, Npad, hpw, img16, 0.125f, attn_prio());
-    else
-      hipLaunchKernelGGL((attention_lc_kernel<T, false>), dim3(grid), dim3(768), lds_lc, s,
-                         (const T*)qkv, (T*)out, B, N, H, Npad, hpw, img16, 0.125f, attn_prio());
-    return hipGetLastError();
-  }
-  if (variant == 20 || (!CAUSAL && variant == 0 && N >= 256 && N <= 259 && 2 * grp16 <= 160 * 1024)) {
-    // phase-locked pair of 8-wave groups, one 16-wave workgroup per CU
-    // (attention_x16_kernel, the default there): the x8 kernel's N range
-    if (CAUSAL || N < 256 || N > 259) return hipErrorInvalidValue;
-    const int img_bytes = img16, grp_bytes = grp16;
-    if (2 * grp_bytes > 160 * 1024) return hipErrorInvalidValue;
-    static bool x16_attr = false;
-    if (!x16_attr) {
-      const hipError_t e = hipFuncSetAttribute((const void*)attention_x16_kernel<T>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               160 * 1024);
-      if (e != hipSuccess) return e;
-      x16_attr = true;
-    }
-    static int ncu16 = [] {
-      int d = 0, n = 0;
-      if (hipGetDevice(&d) != hipSuccess ||
-          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
-        n = 256;
-      return n;
-    }();
-    const int heads = B * H, slots = 2 * ncu16;
-    int hpg = (heads + slots - 1) / slots;
-    hpg = hpg < 1 ? 1 : hpg;
-    const int grid = (heads + 2 * hpg - 1) / (2 * hpg);
-    hipLaunchKernelGGL((attention_x16_kernel<T>), dim3(grid), dim3(1024), 2 * grp_bytes, s,
-                       (const T*)qkv, (T*)out, B, N, H, Npad, hpg, img_bytes, grp_bytes, 0.125f,
-                       attn_prio());
-    return hipGetLastError();
-  }
-  if (variant == 8 || variant == 24 ||
-      (!CAUSAL && variant == 0 && N >= 256 && N < 288 && lds_x8 <= 80 * 1024)) {
+  if (variant == 8 || (!CAUSAL && variant == 0 && N >= 256 && N < 288 && lds_x8 <= 80 * 1024)) {
     // at most 3 ragged queries: one per merging wave (attention_x8_kernel)
     if (CAUSAL || N < 256 || N > 259 || lds_x8 > 80 * 1024) return hipErrorInvalidValue;
     static bool x8_attr = false;
@@ -1738,7 +1097,7 @@ hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, 
     hpw = hpw < 1 ? 1 : hpw;
     const int grid = (heads + hpw - 1) / hpw;
     hipLaunchKernelGGL((attention_x8_kernel<T>), dim3(grid), dim3(512), lds_x8, s, (const T*)qkv,
-                       (T*)out, B, N, H, Npad, hpw, 0.125f, attn_prio(), variant == 24 ? 1 : 0);
+                       (T*)out, B, N, H, Npad, hpw, 0.125f, attn_prio());
     return hipGetLastError();
   }
   // pipelined kernel (default; variant 2): two K/V buffers must fit in LDS
