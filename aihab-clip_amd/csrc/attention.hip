@@ -97,6 +97,38 @@ struct HeadGeom {
     return c;
   }
   static MICLIP_DEV int vinv(int p, int row) { return vswz(p, row); }   // involutions
+  // DH = 80: V's padding chunk 10 holds ones, so O^T row 80 is the P row sum
+  static constexpr bool ONES = DH == 80;
+};
+
+// Head dim 80 with UNPADDED rows (160 B, 10 chunks): the pipelined head-dim-80
+// kernel, whose three half-head K/V slots must fit one CU's LDS beside each other
+// (3 x 40 KiB). K chunks rotated by row bit 4, V chunks by 2 on even rows: by the
+// bank model (MI355X_MICROARCH.md LDS table; the K ds_read_b128 lane groups over
+// rows l32, the V ds_read_b64_tr_b16 groups over rows 4 (g >> 1) + tq (+8, +16))
+// both are conflict-free -- 20 / 24 LDS cycles per tile. The third O^T tile's dims
+// 80-95 do not exist here: its lanes for chunks 10-11 read chunks 8-9 again (same
+// address, a broadcast), so O^T rows 80-95 are copies, never stored, and the row
+// sum is taken on VALU (ONES = false).
+struct HeadGeom80u {
+  static constexpr int NKS = 5, NDT = 3, ROWB = 160, CH = 10, TILEB = 32 * ROWB;
+  static constexpr bool ONES = false;
+  static MICLIP_DEV int kswz(int c, int row) {
+    const int p = c + ((row >> 4) & 1);
+    return p < 10 ? p : p - 10;
+  }
+  static MICLIP_DEV int kinv(int p, int row) {
+    const int c = p - ((row >> 4) & 1);
+    return c >= 0 ? c : c + 10;
+  }
+  static MICLIP_DEV int vswz(int c, int row) {
+    const int p = c + ((row & 1) ? 0 : 2);
+    return p < 10 ? p : p - 10;
+  }
+  static MICLIP_DEV int vinv(int p, int row) {
+    const int c = p - ((row & 1) ? 0 : 2);
+    return c >= 0 ? c : c + 10;
+  }
 };
 
 template <typename T>
@@ -119,12 +151,12 @@ MICLIP_DEV float dot2acc<__bf16>(uint32_t a, uint32_t b, float c) {
 // and O^T (cdna_hip_programming.md T13: the decision precedes the tile's
 // exponentials; the old max is kept while the tile max exceeds it by <= 8, p <=
 // 2^8, exact range for fp16/bf16 P). Leaves P^T as the P.V MFMA's B operand
-// (pf[s2]: accumulator regs 8 s2 .. 8 s2 + 7) and, for DH 64, adds the fp32 row
-// sum to lsum. DH 80: the sum rides the P.V MFMAs (V's padding dims 80-87 are
-// ones: O^T rows 80-87 = sum_k P).
-template <typename T, int DH>
-MICLIP_DEV void softmax_tile(f32x16& sacc, float c2, float& m, float& lsum,
-                             f32x16 (&o)[HeadGeom<DH>::NDT], i16x8 (&pf)[2]) {
+// (pf[s2]: accumulator regs 8 s2 .. 8 s2 + 7) and, with SUMP, adds the fp32 row
+// sum to lsum. Without (padded head dim 80): the sum rides the P.V MFMAs (V's
+// padding dims 80-87 are ones: O^T rows 80-87 = sum_k P).
+template <typename T, int NDT, bool SUMP>
+MICLIP_DEV void softmax_tile(f32x16& sacc, float c2, float& m, float& lsum, f32x16 (&o)[NDT],
+                             i16x8 (&pf)[2]) {
   // a v_max3 tree: 8 ops for 16 values
   const float t0 = fmaxf(fmaxf(sacc[0], sacc[1]), sacc[2]);
   const float t1 = fmaxf(fmaxf(sacc[3], sacc[4]), sacc[5]);
@@ -141,7 +173,7 @@ MICLIP_DEV void softmax_tile(f32x16& sacc, float c2, float& m, float& lsum,
 #pragma unroll
     for (int r = 0; r < 16; ++r)
 #pragma unroll
-      for (int dt = 0; dt < HeadGeom<DH>::NDT; ++dt) o[dt][r] *= alpha;
+      for (int dt = 0; dt < NDT; ++dt) o[dt][r] *= alpha;
   }
   // raw v_exp_f32: exp2f's denormal-range fix-up (cmp/cndmask/ldexp per
   // element) is dead weight here -- results below 2^-126 vanish in the fp16
@@ -155,14 +187,14 @@ MICLIP_DEV void softmax_tile(f32x16& sacc, float c2, float& m, float& lsum,
   for (int r = 0; r < 16; ++r) {
     const float v = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[r], c2, -m));
     sacc[r] = v;
-    if constexpr (DH != 80) {
+    if constexpr (SUMP) {
       if (r < 4)
         ps[r] = v;
       else
         ps[r & 3] += v;
     }
   }
-  if constexpr (DH != 80) lsum += (ps[0] + ps[2]) + (ps[1] + ps[3]);
+  if constexpr (SUMP) lsum += (ps[0] + ps[2]) + (ps[1] + ps[3]);
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -178,13 +210,14 @@ MICLIP_DEV void softmax_tile(f32x16& sacc, float c2, float& m, float& lsum,
 // first / last: a key range processed in several calls starts the online
 // softmax state in the first call and reduces lsum across the lane halves in
 // the last one (both true: one call over the range).
-template <typename T, bool CAUSAL, int DH, bool PIPE = true, bool OPQ = false>
-MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
-                             const i16x8 (&qf)[HeadGeom<DH>::NKS], int chunk, int N, int Npad,
-                             float c2, int lane, f32x16 (&o)[HeadGeom<DH>::NDT], float& lsum,
-                             float& m, int kt0 = 0, int kt_end = -1, int prio = 0,
-                             bool first = true, bool last = true) {
-  using G = HeadGeom<DH>;
+// G: the K/V image geometry (HeadGeom<DH>, or HeadGeom80u); tile0: the key tile
+// held at byte 0 of kimg / vimg (a slot holding tiles tile0.. of the head).
+template <typename T, bool CAUSAL, int DH, bool PIPE = true, bool OPQ = false,
+          class G = HeadGeom<DH>>
+MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg, const i16x8 (&qf)[G::NKS],
+                             int chunk, int N, int Npad, float c2, int lane, f32x16 (&o)[G::NDT],
+                             float& lsum, float& m, int kt0 = 0, int kt_end = -1, int prio = 0,
+                             bool first = true, bool last = true, int tile0 = 0) {
   const int l32 = lane & 31, hh = lane >> 5;
   const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
   const int q = chunk * 32 + l32;
@@ -210,7 +243,8 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
   int voff[G::NDT];
 #pragma unroll
   for (int dt = 0; dt < G::NDT; ++dt) {
-    const int ch = 4 * dt + 2 * (g & 1) + (tp >> 1);
+    int ch = 4 * dt + 2 * (g & 1) + (tp >> 1);
+    if (ch >= G::CH) ch -= 2;   // HeadGeom80u: dims 80-95 re-read 64-79 (never stored)
     voff[dt] = (4 * (g >> 1) + tq) * G::ROWB + (G::vswz(ch, 4 * (g >> 1) + tq) << 4) + 8 * (tp & 1);
   }
   // Two-stage tile pipeline (cdna_hip_programming.md T15): the S^T MFMAs of
@@ -220,16 +254,13 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
   // (prio: every caller passes attn_prio() = 1; the priority raise is unconditional
   // so no per-tile branch on a kernel argument is left in the loop)
   (void)prio;
-  // 32-bit LDS addresses (address space 3) from an opaque wave-uniform base: the
-  // images' base is otherwise re-added to every per-lane offset at every read
-  // (the dynamic-LDS symbol is a relocation hipcc does not fold)
   // 32-bit LDS addresses (address space 3). OPQ: from an opaque wave-uniform base
   // -- the dynamic-LDS symbol is a relocation hipcc otherwise re-adds to every
   // per-lane offset at every read (6 VALU per key tile); it costs registers, so
   // only the x8 kernel (122 of its 128 VGPRs) takes it (the 16-wave
   // attention_kernel<64> spilled with it)
-  unsigned kb = (unsigned)(uintptr_t)(const LDS_AS char*)kimg;
-  unsigned vb = (unsigned)(uintptr_t)(const LDS_AS char*)vimg;
+  unsigned kb = (unsigned)(uintptr_t)(const LDS_AS char*)kimg - tile0 * G::TILEB;
+  unsigned vb = (unsigned)(uintptr_t)(const LDS_AS char*)vimg - tile0 * G::TILEB;
   if constexpr (OPQ) asm("" : "+s"(kb), "+s"(vb));
   const LDS_AS char* kl = (const LDS_AS char*)(uintptr_t)kb;
   const LDS_AS char* vl = (const LDS_AS char*)(uintptr_t)vb;
@@ -258,7 +289,7 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
       }
     }
     i16x8 pf[2];
-    softmax_tile<T, DH>(sacc, c2, m, lsum, o, pf);
+    softmax_tile<T, G::NDT, !G::ONES>(sacc, c2, m, lsum, o, pf);
     // ---- O^T[d][q] += V^T . P^T ----
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -295,7 +326,7 @@ MICLIP_DEV void attend_chunk(const char* kimg, const char* vimg,
       softmax_pv(kt, sa);
     }
   }
-  if constexpr (DH == 80) {
+  if constexpr (G::ONES) {
     // O^T row 80 (hh = 0 lanes) / 84 (hh = 1): both in the ones chunk, so every
     // lane holds its query's sum of the P values the MFMAs used
     if (last) lsum = o[2][8];
@@ -588,6 +619,268 @@ __global__ __launch_bounds__(576) void attention80s_kernel(const T* __restrict__
                                false, true);
     attend_store<T, 80>(o, lsum, chunk, N, out + (size_t)b * N * D + h * 80, D, lane);
   }
+}
+
+// Keys [0, nkeys) of the unpadded 160-B-row images kx / vx (the keys past the 8
+// full tiles, at most 3) for one wave's 32 queries on VALU, continuing
+// attend_chunk's online-softmax state: attend_extra_keys (head dim 64) over the
+// five 16-dim Q fragments and the three O^T tiles (dims 80-95 of the third are
+// copies, left alone). Call attend_chunk with last = false and reduce lsum after.
+template <typename T>
+MICLIP_DEV void attend_extra_keys80u(const char* kx, const char* vx, const i16x8 (&qf)[5],
+                                     f32x16 (&o)[3], float& lsum, float& m, int nkeys, float c2,
+                                     int lane) {
+  const int hh = lane >> 5;
+  for (int k = 0; k < nkeys; ++k) {
+    const char* kr = kx + k * 160;
+    float part = 0.f;
+#pragma unroll
+    for (int st = 0; st < 5; ++st) {
+      const u32x4 kv = *(const u32x4*)(kr + ((2 * st + hh) << 4));
+      const u32x4 qv = __builtin_bit_cast(u32x4, qf[st]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) part = dot2acc<T>(qv[e], kv[e], part);
+      asm volatile("" ::: "memory");
+    }
+    const float score = xor32_sum(part);
+    const float sc = score * c2;
+    if (!__all(sc - m <= 8.0f)) {
+      const float mnew = fmaxf(m, sc);
+      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+      m = mnew;
+      lsum *= alpha;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        o[0][r] *= alpha;
+        o[1][r] *= alpha;
+        o[2][r] *= alpha;
+      }
+    }
+    const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(score, c2, -m));
+    if (hh == 0) lsum += p;
+    const float p16 = to_f<T>(to_t<T>(p));
+    const char* vr = vx + k * 160;
+#pragma unroll
+    for (int dt = 0; dt < 3; ++dt)
+#pragma unroll
+      for (int rq = 0; rq < 4; ++rq) {
+        if (dt == 2 && rq >= 2) continue;   // dims 80-95: none
+        const i16x4 v = *(const i16x4*)(vr + ((4 * dt + rq) << 4) + 8 * hh);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          o[dt][4 * rq + e] = __builtin_fmaf(p16, from_bits<T>(v[e]), o[dt][4 * rq + e]);
+        asm volatile("" ::: "memory");
+      }
+  }
+}
+
+// Head dim 80, pipelined (default at N = 256..259: open_clip ViT-H/14 at 224 px,
+// C5). attention80s_kernel holds a whole head (110 KiB) and so runs one head at a
+// time per CU, fetch then compute: 2.25 waves per SIMD, 9 query chunks over 4
+// SIMDs (one SIMD carries 3), the 257th key as a 31/32-masked ninth tile. Here one
+// workgroup (8 waves, 2 per SIMD: the register budget is 256) walks hpw heads with
+// the K/V images in half-head units (key tiles 0-3, 4-7; 40 KiB of unpadded
+// 160-B rows, HeadGeom80u) in a ring of three slots: while a wave computes unit u,
+// units u + 1 and u + 2 are in flight, so a head's fetch runs under the previous
+// head's MFMAs. Wave w owns query chunk w over the 8 full key tiles, then the keys
+// past them (N - 256 <= 3, staged beside the slots) on VALU; the ragged query chunk
+// (N - 256 queries) is dealt flash-decoding style, key tile w to wave w (waves 0-3
+// in the first half, 4-7 in the second: one of each per SIMD), wave 7 also its
+// extra keys, and wave c merges query c's 8 partials (LDS, fixed order) after the
+// head's closing barrier. Q fragments of the next head load into registers during
+// the second half; hipcc's wait for them at the head boundary also retires the
+// (older) DMAs of the next head. Online-softmax arithmetic per tile as
+// attend_chunk's; the row sum is taken on VALU (no ones chunk in 160-B rows).
+template <typename T>
+__global__ __launch_bounds__(512) void attention80p_kernel(const T* __restrict__ qkv,
+                                                           T* __restrict__ out, int B, int N,
+                                                           int H, int hpw, float qk_scale,
+                                                           int prio) {
+  using G = HeadGeom80u;
+  constexpr int HALFB = 128 * G::ROWB;   // 20 KiB: key tiles 0-3 (or 4-7) of K or V
+  constexpr int SLOTB = 2 * HALFB;       // one unit: K half, then V half
+  constexpr int PSTR = 84;               // partial: 80 dims, m, lsum (+2)
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  char* ximg = smem + 3 * SLOTB;                       // [2 parity][K | V | Q, 1 KiB each]
+  float* part = (float*)(smem + 3 * SLOTB + 6144);     // [2 parity][8 waves][3][PSTR]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nvalid = N - 256;   // ragged queries = keys past the 8 full tiles (0..3)
+  const int D = H * 80, ld = 3 * D;
+  const float c2 = qk_scale * kLog2e;
+  const int bh0 = blockIdx.x * hpw;
+  const int nh = (B * H - bh0) < hpw ? (B * H - bh0) : hpw;
+  if (nh <= 0) return;   // workgroup-uniform
+  auto head_base = [&](int bh) {
+    const int b = bh / H, h = bh - b * H;
+    return qkv + (size_t)b * N * ld + h * 80;
+  };
+  // unit (head at base, half): K and V rows 128 half .. +127 into `slot`, 40
+  // 1-KiB pieces (5 per wave), the swizzle applied to the source chunk
+  // opaque lane index: per-lane offsets are recomputed at each use instead of
+  // hoisted out of the head loop for every inlined call site (which spilled)
+  auto olane = [&]() {
+    int l = lane;
+    asm volatile("" : "+v"(l));
+    return l;
+  };
+  auto stage_half = [&](const T* base, int half, int slot) {
+    char* img = smem + slot * SLOTB;
+    const int lane = olane();
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int pc = wave + 8 * i;
+      const bool isv = pc >= 20;
+      const int piece = isv ? pc - 20 : pc;
+      const int off = piece * 1024 + lane * 16;
+      const int rl = off / G::ROWB, pch = (off - rl * G::ROWB) >> 4;
+      const int row = 128 * half + rl;
+      const int c = isv ? G::vinv(pch, row) : G::kinv(pch, row);
+      glds16_hidden(base + (size_t)row * ld + (isv ? 2 * D : D) + c * 8,
+                    img + (isv ? HALFB : 0) + piece * 1024);
+    }
+  };
+  // rows 256.. (clamped to N - 1; unswizzled 160-B rows) of K (wave 0), V (wave
+  // 1) and Q (wave 2): the keys past the 8 full tiles and the ragged queries
+  auto stage_extra = [&](const T* base, int par) {
+    if (wave < 3) {
+      const int lane = olane();
+      const int off = lane * 16, rl = off / G::ROWB, ch = (off - rl * G::ROWB) >> 4;
+      const int r = 256 + rl < N ? 256 + rl : N - 1;
+      glds16_hidden(base + (size_t)r * ld + (wave == 0 ? D : wave == 1 ? 2 * D : 0) + ch * 8,
+                    ximg + par * 3072 + wave * 1024);
+    }
+  };
+  // the ragged chunk's Q fragments (load_q's layout) from the staged rows: query
+  // lanes past the valid ones read row 0 (finite, never stored)
+  auto ragged_q = [&](i16x8 (&qx)[5], int par) {
+    const int lane = olane();
+    const int l32 = lane & 31, hh = lane >> 5;
+    const char* qrow = ximg + par * 3072 + 2048 + (l32 < nvalid ? l32 : 0) * G::ROWB + hh * 16;
+#pragma unroll
+    for (int s = 0; s < 5; ++s) qx[s] = *(const i16x8*)(qrow + 32 * s);
+  };
+  // this wave's partial of the ragged queries: lane (l32, hh) holds O^T rows d =
+  // (r & 3) + 8 (r >> 2) + 4 hh (+32 dt) of query l32
+  auto put_part = [&](const f32x16 (&ox)[3], float mx, float lx, int par) {
+    const int l32 = lane & 31, hh = lane >> 5;
+    if (l32 < nvalid) {
+      float* pw = part + ((par * 8 + wave) * 3 + l32) * PSTR;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int d = (r & 3) + 8 * (r >> 2) + 4 * hh;
+        pw[d] = ox[0][r];
+        pw[32 + d] = ox[1][r];
+        if (r < 8) pw[64 + d] = ox[2][r];
+      }
+      if (hh == 0) {
+        pw[80] = mx;
+        pw[81] = lx;
+      }
+    }
+  };
+  // wave c < nvalid: ragged query c of head bh from its 8 partials, in wave order;
+  // lane = output dim (lanes 0-15 also dims 64-79)
+  auto merge = [&](int bh, int par) {
+    if (wave < nvalid) {
+      const int b = bh / H, h = bh - b * H;
+      const float* pc = part + (par * 8 * 3 + wave) * PSTR;
+      float mx = -1e30f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) mx = fmaxf(mx, pc[i * 3 * PSTR + 80]);
+      float l = 0.f, a0 = 0.f, a1 = 0.f;
+      const int d1 = 64 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float* pi = pc + i * 3 * PSTR;
+        const float w = __builtin_amdgcn_exp2f(pi[80] - mx);
+        l += w * pi[81];
+        a0 += w * pi[lane];
+        a1 += w * pi[d1];
+      }
+      T* orow = out + ((size_t)b * N + 256 + wave) * D + h * 80;
+      orow[lane] = to_t<T>(a0 / l);
+      if (lane < 16) orow[64 + lane] = to_t<T>(a1 / l);
+    }
+  };
+
+  i16x8 qf[5], qn[5];
+  {
+    const T* base = head_base(bh0);
+    stage_half(base, 0, 0);
+    stage_half(base, 1, 1);
+    if (nvalid > 0) stage_extra(base, 0);
+    load_q<T, 80>(qf, base, ld, wave, N, lane);
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]), "+v"(qf[4])
+                 :
+                 : "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  for (int j = 0; j < nh; ++j) {
+    const int bh = bh0 + j, b = bh / H, h = bh - b * H;
+    const int sa = (2 * j) % 3, sb = (2 * j + 1) % 3, sn = (2 * j + 2) % 3;
+    const bool more = j + 1 < nh;
+    const T* nbase = head_base(more ? bh + 1 : bh);
+    // ---- first half: key tiles 0-3 in slot sa. Unit (j+1, 0) -> slot sn, the
+    // slot of unit (j-1, 1), which every wave left before the barrier above ----
+    if (more) stage_half(nbase, 0, sn);
+    if (j > 0) merge(bh - 1, (j - 1) & 1);
+    const char* ia = smem + sa * SLOTB;
+    // (the ragged tile first and the chunk's stores before the second half's
+    // ragged tile: the two O^T sets are never live together)
+    if (nvalid > 0 && wave < 4) {
+      f32x16 ox[3];
+      float lx, mx;
+      i16x8 qx[5];
+      ragged_q(qx, j & 1);
+      attend_chunk<T, false, 80, true, false, G>(ia, ia + HALFB, qx, 8, N, 256, c2, olane(), ox, lx,
+                                                 mx, wave, wave + 1, prio, true, true, 0);
+      put_part(ox, mx, lx, j & 1);
+    }
+    f32x16 o[3];
+    float lsum, m;
+    attend_chunk<T, false, 80, true, false, G>(ia, ia + HALFB, qf, wave, N, 256, c2, olane(), o, lsum,
+                                               m, 0, 4, prio, true, false, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // ---- second half: key tiles 4-7 in slot sb. Unit (j+1, 1) -> slot sa (just
+    // left), the next head's extra keys (the other parity) and Q fragments ----
+    if (more) {
+      stage_half(nbase, 1, sa);
+      if (nvalid > 0) stage_extra(nbase, (j + 1) & 1);
+      load_q<T, 80>(qn, nbase, ld, wave, N, lane);
+    }
+    const char* ib = smem + sb * SLOTB;
+    const char* ix = ximg + (j & 1) * 3072;
+    attend_chunk<T, false, 80, true, false, G>(ib, ib + HALFB, qf, wave, N, 256, c2, olane(), o, lsum,
+                                               m, 4, 8, prio, false, false, 4);
+    if (nvalid > 0) attend_extra_keys80u<T>(ix, ix + 1024, qf, o, lsum, m, nvalid, c2, olane());
+    lsum = xor32_sum(lsum);
+    if (more) {
+      // hipcc waits for these loads here (vmcnt(0): nothing younger is visible to
+      // it -- the output stores come after), which also retires the next head's
+      // older DMAs before the barrier
+#pragma unroll
+      for (int s = 0; s < 5; ++s) qf[s] = qn[s];
+      asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]), "+v"(qf[4]));
+    }
+    attend_store<T, 80>(o, lsum, wave, N, out + (size_t)b * N * D + h * 80, D, lane);
+    if (nvalid > 0 && wave >= 4) {
+      f32x16 ox[3];
+      float lx, mx;
+      i16x8 qx[5];
+      ragged_q(qx, j & 1);
+      attend_chunk<T, false, 80, true, false, G>(ib, ib + HALFB, qx, 8, N, 256, c2, olane(), ox, lx,
+                                                 mx, wave, wave + 1, prio, true, false, 4);
+      if (wave == 7) attend_extra_keys80u<T>(ix, ix + 1024, qx, ox, lx, mx, nvalid, c2, olane());
+      lx = xor32_sum(lx);
+      put_part(ox, mx, lx, j & 1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  merge(bh0 + nh - 1, (nh - 1) & 1);
 }
 
 
@@ -1043,8 +1336,35 @@ template <typename T, bool CAUSAL>
 hipError_t attn_launch(const void* qkv, void* out, int B, int N, int H, int dh, hipStream_t s,
                        int variant) {
   if (dh == 80) {
-    // the two-phase kernel (default) where a chunk per wave fits 9 waves and Q's
-    // image fits beside K / V; variant 1 = attention_kernel<80>
+    // the pipelined kernel (default; variant 6) at 8 full query chunks + at most 3
+    // more queries; else the two-phase kernel (variant 2) where a chunk per wave fits
+    // 9 waves and Q's image fits beside K / V; variant 1 = attention_kernel<80>
+    if (variant == 6 || (variant == 0 && !CAUSAL && N >= 256 && N <= 259)) {
+      if (CAUSAL || N < 256 || N > 259) return hipErrorInvalidValue;
+      constexpr size_t lds80p = 3 * 2 * 128 * 160 + 6144 + 2 * 8 * 3 * 84 * 4;
+      static bool a80p = false;
+      if (!a80p) {
+        const hipError_t e = hipFuncSetAttribute((const void*)attention80p_kernel<T>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)lds80p);
+        if (e != hipSuccess) return e;
+        a80p = true;
+      }
+      static int ncu80 = [] {
+        int d = 0, n = 0;
+        if (hipGetDevice(&d) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+          n = 256;
+        return n;
+      }();
+      const int heads = B * H;
+      int hpw = (heads + ncu80 - 1) / ncu80;
+      hpw = hpw < 1 ? 1 : hpw;
+      const int grid = (heads + hpw - 1) / hpw;
+      hipLaunchKernelGGL((attention80p_kernel<T>), dim3(grid), dim3(512), lds80p, s, (const T*)qkv,
+                         (T*)out, B, N, H, hpw, 1.0f / sqrtf(80.f), attn_prio());
+      return hipGetLastError();
+    }
     const int Npad = (N + 31) & ~31, nchunks = Npad / 32;
     const size_t lds80 = (size_t)Npad * (2 * HeadGeom<80>::ROWB + 160);
     if (!CAUSAL && variant != 1 && nchunks <= 9 && Npad >= 160 && lds80 <= 160 * 1024) {

@@ -255,9 +255,9 @@ int64_t miclip_model_bytes(const miclip_model* m);
 int miclip_model_flags(const miclip_model* m);
 /* Diagnostics: the GEMM kernel of the block launches (>= 256 rows) --
  * which 0: the folded-LN store GEMMs (QKV, c_fc), 1: the fp16 residual GEMMs
- * (out-proj, c_proj); variant 0 (default) / 259 (the 8-wave persistent kernel) /
- * 508, 516 (the 4-wave gemm4s kernel); which 2: the MX-fp8 GEMMs (variants of
- * miclip_op_gemm_mx_v). All are bit-identical, so results never change;
+ * (out-proj, c_proj); variant 0 (default) / 259 (the 8-wave persistent kernel);
+ * which 2: the MX-fp8 GEMMs (variants of miclip_op_gemm_mx_v). All are
+ * bit-identical, so results never change;
  * bench.py --ab-gemm times them in one process. */
 int miclip_set_gemm_variant(miclip_model* m, int32_t which, int32_t variant);
 /* Switches a run-time option of a handle (only MICLIP_OPT_FULL_LAST_BLOCK; the
@@ -339,10 +339,14 @@ int miclip_op_layernorm(int32_t dtype, const void* in, const float* gamma, const
  * buffer, out [B*N, H*dh]; replaces F.scaled_dot_product_attention inside
  * nn.MultiheadAttention (clip/model.py:179-181), causal = text mask (323-329).
  * head_dim dh: 64, or 80 (open_clip ViT-H/14 vision tower); 0 means 64.
- * variant (dh 64): 0 = default (pipelined multi-head kernel for N <= 320, else
- * one head per workgroup), 1 = one head per workgroup, 2 = pipelined,
- * 4 = pipelined with the last-chunk split. dh 80 always runs one head per
- * workgroup (N <= 416). */
+ * variant (dh 64): 0 = default (two workgroups per CU at N = 256..259, else the
+ * pipelined multi-head kernel for N <= 320, else one head per workgroup), 1 = one
+ * head per workgroup, 2 = pipelined, 4 = pipelined with the last-chunk split,
+ * 8 = two workgroups per CU, 10..16 = one head per workgroup on that many waves.
+ * variant (dh 80): 0 = default (6 at N = 256..259, else 2 where it applies, else
+ * 1), 1 = one head per workgroup (N <= 416), 2 = two-phase fetch (N = 160..288),
+ * 6 = pipelined half-head K/V ring (N = 256..259). A variant outside its range
+ * fails (never silently replaced). */
 int miclip_op_attention(int32_t dtype, const void* qkv, void* out, int32_t B, int32_t N,
                         int32_t H, int32_t head_dim, int32_t causal, int32_t variant,
                         void* stream);

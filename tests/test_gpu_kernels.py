@@ -357,9 +357,10 @@ def test_attention_dh80(lib, dt, B, N, H, causal):
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
 @pytest.mark.parametrize("B,N,H", [(2, 257, 16), (3, 160, 4), (1, 288, 2), (4, 200, 3), (64, 257, 16)])
 def test_attention_dh80_two_phase_bitexact(lib, dt, B, N, H):
-    """The two-phase head-dim-80 kernel (default, variant 2: Q by LDS-DMA, key tiles 0-3
-    computed while the rest lands) equals attention_kernel<80> (variant 1) bit for bit;
-    outside its range (N < 129 or > 288, causal) variant 2 is refused, not replaced."""
+    """The two-phase head-dim-80 kernel (variant 2: Q by LDS-DMA, key tiles 0-3
+    computed while the rest lands; the default outside N = 256..259) equals
+    attention_kernel<80> (variant 1) bit for bit; outside its range (N < 129 or > 288,
+    causal) variant 2 is refused, not replaced."""
     code, tdt = DT[dt]
     g = torch.Generator(device="cuda").manual_seed(B * 1000 + N + H + 801)
     qkv = (torch.randn(B * N, 3 * H * 80, device="cuda", generator=g) * 1.5).to(tdt)
@@ -370,13 +371,61 @@ def test_attention_dh80_two_phase_bitexact(lib, dt, B, N, H):
                                             v, _stream()))
         outs.append(out)
     torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+    assert torch.equal(outs[0], outs[1])
+    if not 256 <= N <= 259:   # there the default is the pipelined kernel (variant 6)
+        assert torch.equal(outs[1], outs[2])
     assert bool((outs[1][B * N] == 7.0).all())
     for bad_n, causal in ((100, 0), (300, 0), (257, 1)):
         x = torch.zeros(bad_n, 3 * 80, device="cuda", dtype=tdt)
         y = torch.zeros(bad_n, 80, device="cuda", dtype=tdt)
         assert lib.miclip_op_attention(code, x.data_ptr(), y.data_ptr(), 1, bad_n, 1, 80, causal, 2,
                                        _stream()) != 0
+
+
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+@pytest.mark.parametrize("N", [256, 257, 258, 259])
+def test_attention_dh80_pipelined(lib, dt, N):
+    """The pipelined head-dim-80 kernel (variant 6, the default at N = 256..259: one
+    workgroup walks hpw heads through a ring of three half-head K/V slots, the keys
+    past the 8 full tiles on VALU, the ragged queries merged from 8 per-wave partials).
+    Against the fp32 reference with hpw = 1 (16 heads) and hpw = 9 (2304 heads over 256
+    CUs); every head's arithmetic is independent of hpw, so the whole batch must equal
+    launches of 16 images (256 heads: hpw = 1) bit for bit, on every one of several
+    repeats (a slot or partial race would vary run to run). Canary row past the output:
+    the padding dims are never stored. Refused when causal or outside N = 256..259."""
+    code, tdt = DT[dt]
+    H = 16
+    tol = 4e-2 if dt == "bf16" else 6e-3
+    g = torch.Generator(device="cuda").manual_seed(N + 8080)
+    small = (torch.randn(1 * N, 3 * H * 80, device="cuda", generator=g) * 1.5).to(tdt)
+    out = torch.full((N + 1, H * 80), 7.0, device="cuda", dtype=tdt)
+    _check(lib, lib.miclip_op_attention(code, small.data_ptr(), out.data_ptr(), 1, N, H, 80, 0, 6,
+                                        _stream()))
+    torch.cuda.synchronize()
+    assert (out[:N].float() - _attn_ref(small, 1, N, H, 0, dh=80)).abs().max().item() < tol
+    assert bool((out[N] == 7.0).all())
+    B = 144                                  # 2304 heads: hpw = 9 on 256 CUs
+    qkv = (torch.randn(B * N, 3 * H * 80, device="cuda", generator=g) * 1.5).to(tdt)
+    ref = torch.empty(B * N, H * 80, device="cuda", dtype=tdt)
+    per, esz = 16, ref.element_size()
+    for b0 in range(0, B, per):
+        _check(lib, lib.miclip_op_attention(code, qkv.data_ptr() + b0 * N * 3 * H * 80 * esz,
+                                            ref.data_ptr() + b0 * N * H * 80 * esz, per, N, H, 80,
+                                            0, 6, _stream()))
+    torch.cuda.synchronize()
+    want = _attn_ref(qkv[:4 * N], 4, N, H, 0, dh=80)
+    assert (ref[:4 * N].float() - want).abs().max().item() < tol
+    big = torch.empty(B * N + 1, H * 80, device="cuda", dtype=tdt)
+    for _ in range(3):
+        big.fill_(7.0)
+        _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), big.data_ptr(), B, N, H, 80, 0, 0,
+                                            _stream()))
+        torch.cuda.synchronize()
+        assert torch.equal(big[:B * N], ref), f"{(big[:B * N] != ref).sum().item()} elements differ"
+        assert bool((big[B * N] == 7.0).all())
+    for bad_n, causal in ((255, 0), (260, 0), (257, 1)):
+        assert lib.miclip_op_attention(code, qkv.data_ptr(), big.data_ptr(), 1, bad_n, H, 80, causal,
+                                       6, _stream()) != 0
 
 
 @pytest.mark.parametrize("dt", ["fp16", "bf16"])
