@@ -49,7 +49,17 @@ diag: $(OBJS)
 	$(HIPCC) $(HIPFLAGS) -DMICLIP_DIAG_SKIP_LNSTATS -c $(SRC_DIR)/norm.hip -o $(DIAG_DIR)/norm_nolns.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(DIAG_DIR)/norm_nolns.o $(filter-out $(OBJ_DIR)/norm.o,$(OBJS)) -o $(DIAG_DIR)/libmiclip_nolns.so
 
+# timing diagnostic: the persistent GEMM with 16 / 32 / 64 registers held live across
+# its main loop (MICLIP_DIAG_STASH; outputs unchanged), pricing a deferred-epilogue stash
+diag-stash: $(OBJS)
+	@mkdir -p $(DIAG_DIR)
+	for n in 16 32 64; do \
+	  $(HIPCC) $(HIPFLAGS) -DMICLIP_DIAG_STASH=$$n -c $(SRC_DIR)/gemm.hip -o $(DIAG_DIR)/gemm_stash$$n.o && \
+	  $(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(DIAG_DIR)/gemm_stash$$n.o $(filter-out $(OBJ_DIR)/gemm.o,$(OBJS)) -o $(DIAG_DIR)/libmiclip_stash$$n.so || exit 1; \
+	  $(HIPCC) $(HIPFLAGS) -DMICLIP_DIAG_STASH=$$n --cuda-device-only -S $(SRC_DIR)/gemm.hip -o $(DIAG_DIR)/gemm_stash$$n.s || exit 1; \
+	done
+
 clean:
 	rm -rf build $(LIB)
 
-.PHONY: all clean asm stamps diag
+.PHONY: all clean asm stamps diag diag-stash

@@ -1037,6 +1037,15 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
 
   int prev_stores = -1;   // -1: first tile (full prologue)
   int id = blockIdx.x;
+#ifdef MICLIP_DIAG_STASH
+  // timing diagnostic (make diag-stash, outputs unchanged): MICLIP_DIAG_STASH
+  // registers held live across every K-tile of the main loop, as the stash of a
+  // deferred epilogue (the next tile's K loop finishing this tile's activation
+  // and stores) would be -- prices the register budget of that design
+  float stash[MICLIP_DIAG_STASH];
+#pragma unroll
+  for (int i = 0; i < MICLIP_DIAG_STASH; ++i) asm volatile("v_mov_b32 %0, %1" : "=v"(stash[i]) : "v"(i));
+#endif
   MICLIP_STAMP_BEGIN;
   if (id < ndp) sources(id, m0, n0, asrc, bsrc);
   for (; id < ndp; id += gridDim.x) {
@@ -1098,6 +1107,12 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
       const char* sB1 = smem + (buf * 4 + 3) * HALF + boff;
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
+#ifdef MICLIP_DIAG_STASH
+        if (p == 0) {
+#pragma unroll
+          for (int i = 0; i < MICLIP_DIAG_STASH; ++i) asm volatile("" : "+v"(stash[i]));
+        }
+#endif
         if (p == 0 && wr == 0 && t > 0) {
           MICLIP_KSTAMP(1);
           if (t + 1 < nk)
@@ -1424,6 +1439,10 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
     prev_stores = full ? EpiStores<Epi, TR>::n * RB / 4 : 0;
     MICLIP_STAMP(3);              // epilogue
   }
+#ifdef MICLIP_DIAG_STASH
+#pragma unroll
+  for (int i = 0; i < MICLIP_DIAG_STASH; ++i) asm volatile("" ::"v"(stash[i]));
+#endif
   // the row tail on the same workgroups
   for (int task = blockIdx.x; task < ntail; task += gridDim.x) {
     lds_barrier();

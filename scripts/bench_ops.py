@@ -62,6 +62,10 @@ def main():
         # out / proj: epilogue 4 = the fp16 residual stream of the fp16 model
         shapes = [("qkv", 3 * W, W, 0, 0), ("out", W, W, 4, 0), ("fc", 4 * W, W, 0, 1),
                   ("proj", W, 4 * W, 4, 0)]
+        # (--only fc_noact: the c_fc shape without its QuickGELU, pricing the activation)
+        shapes.append(("fc_noact", 4 * W, W, 0, 0))
+        if not args.only:
+            shapes = shapes[:4]
         if args.ksweep:
             shapes = [(f"k{k}_e{e}", 4 * W, k, e, 0) for e in (3, 0, 2) for k in (256, 1024, 4096)]
         if args.only:
