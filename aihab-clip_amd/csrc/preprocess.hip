@@ -13,7 +13,7 @@
 //     FP contraction off, in Resample.c's operation order (the same doubles
 //     the CPU computes), normalised to 22-bit fixed point; the handle caches
 //     them (PreCache);
-//   * `preprocess_kernel`, one workgroup per (image, band of 16 crop rows):
+//   * `preprocess_kernel`, one workgroup per (image, band of 24 crop rows):
 //     horizontal pass over the input rows the band's vertical taps need x
 //     crop columns -> clip8 -> uint8 rows in LDS; vertical pass from LDS ->
 //     clip8 -> float32 x/255, (x-mean)/std written planar [B,3,n,n] (or the
@@ -36,7 +36,7 @@ namespace miclip {
 namespace {
 
 constexpr int kPB = 22;          // Resample.c PRECISION_BITS = 32 - 8 - 2
-constexpr int kBand = 16;        // crop rows per workgroup
+constexpr int kBand = 24;        // crop rows per workgroup (16: +4 % redundant horizontal rows)
 constexpr int kThreads = 1024;   // 16 waves: the horizontal pass is load-latency bound
 constexpr int kTmpBytes = 96 * 1024;   // LDS staging of horizontally resampled rows
 constexpr int kMaxTaps = 64;
