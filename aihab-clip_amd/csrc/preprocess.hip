@@ -36,7 +36,7 @@ namespace miclip {
 namespace {
 
 constexpr int kPB = 22;          // Resample.c PRECISION_BITS = 32 - 8 - 2
-constexpr int kBand = 24;        // crop rows per workgroup (16: +4 % redundant horizontal rows)
+constexpr int kBand = 24;        // crop rows per workgroup (fewer shared input rows than 16)
 constexpr int kThreads = 1024;   // 16 waves: the horizontal pass is load-latency bound
 constexpr int kTmpBytes = 96 * 1024;   // LDS staging of horizontally resampled rows
 constexpr int kMaxTaps = 64;
