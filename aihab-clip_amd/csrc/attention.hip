@@ -727,6 +727,7 @@ __global__ __launch_bounds__(512) void attention80p_kernel(const T* __restrict__
   auto stage_half = [&](const T* base, int half, int slot) {
     char* img = smem + slot * SLOTB;
     const int lane = olane();
+    const u32x4s desc = make_buffer_desc(base);   // 32-bit offsets from the head's row 0
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
       const int pc = wave + 8 * i;
@@ -736,7 +737,7 @@ __global__ __launch_bounds__(512) void attention80p_kernel(const T* __restrict__
       const int rl = off / G::ROWB, pch = (off - rl * G::ROWB) >> 4;
       const int row = 128 * half + rl;
       const int c = isv ? G::vinv(pch, row) : G::kinv(pch, row);
-      glds16_hidden(base + (size_t)row * ld + (isv ? 2 * D : D) + c * 8,
+      blds16_hidden(desc, (unsigned)(row * ld + (isv ? 2 * D : D) + c * 8) * (unsigned)sizeof(T),
                     img + (isv ? HALFB : 0) + piece * 1024);
     }
   };
@@ -1081,14 +1082,17 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
     const int bh = bh0 + j, b = bh / H, h = bh - b * H;
     const T* base = head_base(bh);
     // every wave finished reading the previous head's K/V (the closing barrier
-    // below: the extra keys are taken before it) before these DMAs overwrite them
+    // below: the extra keys are taken before it) before these DMAs overwrite them.
+    // buffer_load ... lds from a per-head resource: 32-bit offsets (rows clamped, so
+    // always inside the image) instead of a 64-bit address product per piece
+    const u32x4s desc = make_buffer_desc(base);
     for (int pc = wave; pc < 2 * pieces; pc += 8) {
       const bool isv = pc >= pieces;
       const int piece = isv ? pc - pieces : pc;
       const int row = piece * 8 + prow;
       const int r = row < N ? row : N - 1;   // pad rows: finite data, masked keys
       const int lch = isv ? (pch ^ ((row & 3) << 1)) : (pch ^ ((row >> 1) & 7));
-      glds16_hidden(base + (size_t)r * ld + (isv ? 2 * D : D) + lch * 8,
+      blds16_hidden(desc, (unsigned)(r * ld + (isv ? 2 * D : D) + lch * 8) * (unsigned)sizeof(T),
                     (isv ? vimg : kimg) + piece * 1024);
     }
     MICLIP_STAMP(6);   // DMA issue

@@ -184,6 +184,30 @@ MICLIP_DEV void glds16_hidden(const void* g, const void* lds) {
       : "memory");
 }
 
+// The same DMA through a buffer resource (hidden from hipcc's waitcnt pass like
+// glds16_hidden): `desc` is a raw buffer descriptor in SGPRs (make_buffer_desc),
+// `voff` a per-lane 32-bit byte offset -- one VGPR per source instead of a 64-bit
+// address per piece. `lds` must be wave-uniform.
+typedef unsigned int u32x4s __attribute__((ext_vector_type(4)));
+MICLIP_DEV u32x4s make_buffer_desc(const void* base) {
+  const unsigned long long a = (unsigned long long)base;
+  u32x4s d = {(unsigned)a, (unsigned)(a >> 32) & 0xffffu, 0x7fffffffu, 0x00020000u};
+  d[0] = __builtin_amdgcn_readfirstlane(d[0]);
+  d[1] = __builtin_amdgcn_readfirstlane(d[1]);
+  return d;
+}
+MICLIP_DEV void blds16_hidden(u32x4s desc, unsigned voff, const void* lds) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane(
+      (unsigned)(size_t)(const LDS_AS void*)lds);
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(desc), "s"(dst)
+      : "memory");
+}
+
 // Grouped tile order: consecutive ids walk `gm` tile-rows column by column, so
 // the tiles one XCD runs together share A panels and W panels in its L2
 // (ids are already XCD-contiguous after xcd_remap). gm <= 1: row-major.
