@@ -1085,14 +1085,13 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
     // below: the extra keys are taken before it) before these DMAs overwrite them.
     // buffer_load ... lds from a per-head resource: 32-bit offsets (rows clamped, so
     // always inside the image) instead of a 64-bit address product per piece
-    const u32x4s desc = make_buffer_desc(base);
     for (int pc = wave; pc < 2 * pieces; pc += 8) {
       const bool isv = pc >= pieces;
       const int piece = isv ? pc - pieces : pc;
       const int row = piece * 8 + prow;
       const int r = row < N ? row : N - 1;   // pad rows: finite data, masked keys
       const int lch = isv ? (pch ^ ((row & 3) << 1)) : (pch ^ ((row >> 1) & 7));
-      blds16_hidden(desc, (unsigned)(r * ld + (isv ? 2 * D : D) + lch * 8) * (unsigned)sizeof(T),
+      glds16_hidden(base + (unsigned)(r * ld + (isv ? 2 * D : D) + lch * 8),
                     (isv ? vimg : kimg) + piece * 1024);
     }
     MICLIP_STAMP(6);   // DMA issue
