@@ -1194,6 +1194,18 @@ int miclip_op_attention(int32_t dtype, const void* qkv, void* out, int32_t B, in
   return 0;
 }
 
+int miclip_op_im2col(int32_t dtype, int32_t image_dtype, const void* images, void* patches,
+                     int32_t B, int32_t R, int32_t P, int32_t Kp, int32_t variant, void* stream) {
+  if (!images || !patches) return fail(MICLIP_EINVAL, "null argument");
+  if (dtype != MICLIP_FP16 && dtype != MICLIP_BF16) return fail(MICLIP_EINVAL, "bad dtype");
+  if (image_dtype != MICLIP_F32 && image_dtype != MICLIP_FP16 && image_dtype != MICLIP_BF16)
+    return fail(MICLIP_EINVAL, "bad image dtype");
+  const int in_dt = image_dtype == MICLIP_F32 ? kIn32 : image_dtype == MICLIP_FP16 ? kF16 : kBF16;
+  MICLIP_HIP(im2col(dtype == MICLIP_FP16 ? kF16 : kBF16, in_dt, images, patches, B, R, P, Kp,
+                    (hipStream_t)stream, variant));
+  return 0;
+}
+
 int64_t miclip_mx_scale_bytes(int32_t rows, int32_t K) {
   return rows < 1 || K < 128 ? 0 : (int64_t)mx_scale_bytes(rows, K);
 }

@@ -41,6 +41,81 @@ __global__ __launch_bounds__(256) void im2col_kernel(const I* __restrict__ img,
   }
 }
 
+// Band form (the default): one workgroup per (image, patch row py). The band's image
+// rows py*P .. py*P+P-1 of one channel are ONE contiguous run of P*R elements, so the
+// workgroup reads its 3 runs as 4-element vectors (16-B fp32 / 8-B fp16 loads, each
+// wave a contiguous 1-KiB / 512-B span; the per-patch kernel above reads one element
+// per lane at a P-element stride) and writes each of its g patch rows whole (all three
+// channels and the zero pad columns K .. Kp-1). R % 4 == 0 keeps a vector inside one
+// image row; its 4 pixels are then PM-aligned runs of one patch row: PM = 4 (P % 4 ==
+// 0: one 8-B store), 2 (even P, ViT-L/14: two 4-B stores), 1 (odd P: element stores).
+// Same conversion per element as im2col_kernel (bit-identical patches).
+template <typename T, typename I, int PM>
+__global__ __launch_bounds__(256) void im2col_band_kernel(const I* __restrict__ img,
+                                                          T* __restrict__ patches, int R, int P,
+                                                          int Kp) {
+  const int g = R / P, PP = P * P, K = 3 * PP;
+  const int b = blockIdx.x / g, py = blockIdx.x - b * g;
+  const int run = P * R, nv = run / 4;
+  T* dst0 = patches + ((size_t)b * g + py) * g * Kp;   // patch (b, py, 0)
+  const I* src0 = img + (size_t)b * 3 * R * R + (size_t)py * run;
+  constexpr int U = 4;   // vectors in flight per lane
+  for (int f0 = 0; f0 < 3 * nv; f0 += 256 * U) {
+    float v[U][4];
+    int fi[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      fi[u] = f0 + u * 256 + (int)threadIdx.x;
+      const int f = fi[u] < 3 * nv ? fi[u] : 0;
+      const int c = f / nv, i = (f - c * nv) * 4;
+      const I* p = src0 + (size_t)c * R * R + i;
+      if constexpr (sizeof(I) == 4) {
+        const float4 x = *(const float4*)p;
+        v[u][0] = x.x; v[u][1] = x.y; v[u][2] = x.z; v[u][3] = x.w;
+      } else {
+        const u32x2 x = *(const u32x2*)p;
+        const I* e = (const I*)&x;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[u][k] = to_f<I>(e[k]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (fi[u] >= 3 * nv) continue;
+      const int c = fi[u] / nv, i = (fi[u] - c * nv) * 4;
+      const int y = i / R, x = i - y * R;
+      T o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = to_t<T>(v[u][k]);
+      if constexpr (PM == 4) {
+        const int px = x / P, kx = x - px * P;
+        u32x2 w;
+        __builtin_memcpy(&w, o, 8);
+        *(u32x2*)(dst0 + (size_t)px * Kp + c * PP + y * P + kx) = w;
+      } else if constexpr (PM == 2) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int xx = x + 2 * h, px = xx / P, kx = xx - px * P;
+          unsigned w;
+          __builtin_memcpy(&w, o + 2 * h, 4);
+          *(unsigned*)(dst0 + (size_t)px * Kp + c * PP + y * P + kx) = w;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int xx = x + k, px = xx / P, kx = xx - px * P;
+          dst0[(size_t)px * Kp + c * PP + y * P + kx] = o[k];
+        }
+      }
+    }
+  }
+  const int pad = Kp - K;
+  for (int e = threadIdx.x; e < g * pad; e += 256) {
+    const int px = e / pad;
+    dst0[(size_t)px * Kp + K + (e - px * pad)] = to_t<T>(0.f);
+  }
+}
+
 // One wave per workgroup: which XCD it runs on, the shader-clock counter
 // (s_memtime: free-running at the core clock) and the 100 MHz real-time
 // counter. bench.py launches it on the timed stream before and after the timed
@@ -316,10 +391,36 @@ hipError_t row_l2norm(float* x, int R, int D, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <typename T, typename I>
+static void im2col_band(const void* img, T* patches, int B, int R, int P, int Kp, hipStream_t s) {
+  const dim3 grid(B * (R / P));
+  if (P % 4 == 0)
+    hipLaunchKernelGGL((im2col_band_kernel<T, I, 4>), grid, dim3(256), 0, s, (const I*)img, patches,
+                       R, P, Kp);
+  else if (P % 2 == 0)
+    hipLaunchKernelGGL((im2col_band_kernel<T, I, 2>), grid, dim3(256), 0, s, (const I*)img, patches,
+                       R, P, Kp);
+  else
+    hipLaunchKernelGGL((im2col_band_kernel<T, I, 1>), grid, dim3(256), 0, s, (const I*)img, patches,
+                       R, P, Kp);
+}
+
+// variant 0: the band kernel where it applies (R % 4 == 0, Kp % 4 == 0: every vector
+// load and store aligned), else the per-patch kernel; 1: the per-patch kernel
 template <typename T>
 static hipError_t im2col_t(int in_dtype, const void* img, T* patches, int B, int R, int P, int Kp,
-                           hipStream_t s) {
+                           hipStream_t s, int variant) {
   const int np = (R / P) * (R / P);
+  if (variant == 0 && R % 4 == 0 && Kp % 4 == 0 && (in_dtype == kIn32 || in_dtype == kF16 ||
+                                                    in_dtype == kBF16)) {
+    if (in_dtype == kIn32)
+      im2col_band<T, float>(img, patches, B, R, P, Kp, s);
+    else if (in_dtype == kF16)
+      im2col_band<T, _Float16>(img, patches, B, R, P, Kp, s);
+    else
+      im2col_band<T, __bf16>(img, patches, B, R, P, Kp, s);
+    return hipGetLastError();
+  }
   if (in_dtype == kIn32)
     hipLaunchKernelGGL((im2col_kernel<T, float>), dim3(B * np), dim3(256), 0, s,
                        (const float*)img, patches, R, P, Kp);
@@ -341,10 +442,11 @@ hipError_t clock_probe(unsigned long long* out, int n_wg, hipStream_t s) {
 }
 
 hipError_t im2col(int dtype, int in_dtype, const void* img, void* patches, int B, int R, int P,
-                  int Kp, hipStream_t s) {
-  if (B < 1 || P < 1 || R % P || Kp < 3 * P * P) return hipErrorInvalidValue;
-  if (dtype == kF16) return im2col_t(in_dtype, img, (_Float16*)patches, B, R, P, Kp, s);
-  return im2col_t(in_dtype, img, (__bf16*)patches, B, R, P, Kp, s);
+                  int Kp, hipStream_t s, int variant) {
+  if (B < 1 || P < 1 || R % P || Kp < 3 * P * P || variant < 0 || variant > 1)
+    return hipErrorInvalidValue;
+  if (dtype == kF16) return im2col_t(in_dtype, img, (_Float16*)patches, B, R, P, Kp, s, variant);
+  return im2col_t(in_dtype, img, (__bf16*)patches, B, R, P, Kp, s, variant);
 }
 
 hipError_t class_token(const float* cls, const float* pos, void* X, int B, int ntok, int D,

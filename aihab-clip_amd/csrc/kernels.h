@@ -111,9 +111,10 @@ hipError_t attention_q0(int dtype, const void* qkv, void* out, int B, int N, int
 hipError_t gather_rows(const void* src, void* dst, int R, int stride_rows, int D, int elt_bytes,
                        hipStream_t s);
 // images [B,3,R,R] (in_dtype: kIn32 fp32, kF16, kBF16) -> patches [B*g*g, Kp] compute
-// dtype, col = c*P*P + ky*P + kx, zero-padded up to Kp (multiple of 64).
+// dtype, col = c*P*P + ky*P + kx, zero-padded up to Kp (multiple of 64). variant 0:
+// one workgroup per band of patches (vector loads) where R % 4 == 0, 1: one per patch.
 hipError_t im2col(int dtype, int in_dtype, const void* img, void* patches, int B, int R, int P,
-                  int Kp, hipStream_t s);
+                  int Kp, hipStream_t s, int variant = 0);
 // Clock probe: n_wg one-wave workgroups each store {HW_REG_XCC_ID, s_memtime,
 // s_memrealtime, 0} (4 x u64) to out[4 * blockIdx.x ..].
 hipError_t clock_probe(unsigned long long* out, int n_wg, hipStream_t s);

@@ -43,7 +43,7 @@ EXPORTS = (
     "miclip_model_destroy", "miclip_last_error", "miclip_abi_version",
     "miclip_model_bytes", "miclip_model_flags", "miclip_model_set_option", "miclip_set_gemm_variant", "miclip_set_profiling", "miclip_profile_read", "miclip_set_splits", "miclip_image_splits",
     "miclip_op_gemm", "miclip_op_gemm_splitk", "miclip_op_ln_stats", "miclip_op_ln_fold", "miclip_op_gemm_ln",
-    "miclip_op_layernorm", "miclip_op_attention", "miclip_op_attention_q0", "miclip_preprocess",
+    "miclip_op_layernorm", "miclip_op_attention", "miclip_op_attention_q0", "miclip_op_im2col", "miclip_preprocess",
     "miclip_row_norms", "miclip_class_centroids", "miclip_proto_scores",
     "miclip_mx_scale_bytes", "miclip_op_quant_mx", "miclip_op_gemm_mx", "miclip_op_gemm_mx_v", "miclip_op_layernorm_mx",
 )
@@ -117,6 +117,7 @@ def load_library(path: str = None):
         "miclip_op_gemm": ([i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp], ctypes.c_int),
         "miclip_op_layernorm": ([i32, vp, vp, vp, vp, i32, i32, i32, vp], ctypes.c_int),
         "miclip_op_attention_q0": ([i32, vp, vp, i32, i32, i32, i32, vp], ctypes.c_int),
+        "miclip_op_im2col": ([i32, i32, vp, vp, i32, i32, i32, i32, i32, vp], ctypes.c_int),
         "miclip_op_ln_stats": ([vp, vp, i32, i32, vp, vp], ctypes.c_int),
         "miclip_op_ln_fold": ([i32, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, vp], ctypes.c_int),
         "miclip_op_gemm_splitk": ([i32, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32,

@@ -351,6 +351,14 @@ int miclip_op_attention(int32_t dtype, const void* qkv, void* out, int32_t B, in
                         int32_t H, int32_t head_dim, int32_t causal, int32_t variant,
                         void* stream);
 
+/* conv1 patchify as the patch GEMM's A operand (clip/model.py:217-219): images
+ * [B, 3, R, R] (image_dtype MICLIP_F32 / FP16 / BF16) -> patches [B*(R/P)^2, Kp]
+ * (dtype FP16 / BF16), column c*P*P + ky*P + kx, zero up to Kp (>= 3*P*P). variant 0 =
+ * default (one workgroup per band of R/P patches where R % 4 == 0 and Kp % 4 == 0, else
+ * 1), 1 = one workgroup per patch. Bit-identical. */
+int miclip_op_im2col(int32_t dtype, int32_t image_dtype, const void* images, void* patches,
+                     int32_t B, int32_t R, int32_t P, int32_t Kp, int32_t variant, void* stream);
+
 /* Attention of the first query (token row 0, CLS) of every image only, same qkv
  * layout as miclip_op_attention; out [B, H*dh] compact (row b = image b's CLS
  * row). The vision tower's last block (only its CLS rows reach ln_post,

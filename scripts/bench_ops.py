@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--only", default="", help="comma list of gemm shape names to run")
     ap.add_argument("--attn-variants", default="", help="comma list of attention variants")
     ap.add_argument("--torch", action="store_true", help="also time torch.nn.functional.linear")
+    ap.add_argument("--res", type=int, default=224, help="image side (im2col)")
+    ap.add_argument("--patch", type=int, default=14, help="patch side (im2col)")
     args = ap.parse_args()
     lib = _lib.load_library()
     s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -137,6 +139,20 @@ def main():
         ms = timeit(fl_, args.iters)
         out.append(dict(op="layernorm", M=M, D=W, ms=round(ms, 4), gbs=round(M * W * 6 / ms / 1e6, 1)))
         print(json.dumps(out[-1]), flush=True)
+    if "im2col" in args.ops:
+        R, P = args.res, args.patch
+        Kp = (3 * P * P + 63) // 64 * 64
+        img = torch.randn(args.batch, 3, R, R, device="cuda", generator=g)
+        pt = torch.empty(args.batch * (R // P) ** 2, Kp, device="cuda", dtype=dt)
+        for v in (0, 1, 0, 1, 0, 1):
+            def fi():
+                assert lib.miclip_op_im2col(0, 3, img.data_ptr(), pt.data_ptr(), args.batch, R, P, Kp,
+                                            v, s) == 0
+            ms = timeit(fi, args.iters)
+            by = img.numel() * 4 + pt.numel() * 2
+            out.append(dict(op="im2col", variant=v, B=args.batch, R=R, P=P, ms=round(ms, 4),
+                            gbs=round(by / ms / 1e6, 1)))
+            print(json.dumps(out[-1]), flush=True)
 
 
 if __name__ == "__main__":

@@ -508,3 +508,39 @@ def test_gemm_residual_fp16_rounding_bitexact(lib, M, N, K, variant):
                                    M, N, K, 4, 0, variant, _stream()))
     torch.cuda.synchronize()
     assert torch.equal(X, ref), f"{(X != ref).sum().item()} elements differ"
+
+
+# images [B, 3, R, R] -> patches [B*g*g, Kp] (conv1 as a GEMM operand, clip/model.py:217-219)
+@pytest.mark.parametrize("B,R,P", [(3, 224, 32), (2, 224, 14), (2, 336, 14), (2, 224, 16),
+                                   (2, 36, 9), (2, 42, 14), (1, 28, 28)])
+@pytest.mark.parametrize("img_dt", [(3, torch.float32), (0, torch.float16), (1, torch.bfloat16)])
+@pytest.mark.parametrize("dt", ["fp16", "bf16"])
+def test_im2col_band_vs_per_patch_and_unfold(lib, B, R, P, img_dt, dt):
+    code, tdt = DT[dt]
+    icode, idt = img_dt
+    g = torch.Generator(device="cuda").manual_seed(B * 1000 + R * 10 + P)
+    img = torch.randn(B, 3, R, R, device="cuda", generator=g).to(idt)
+    gg, K = R // P, 3 * P * P
+    Kp = (K + 63) // 64 * 64
+    # torch reference: each patch's (c, ky, kx) values in that order, zero pad to Kp
+    ref = torch.zeros(B * gg * gg, Kp, device="cuda", dtype=tdt)
+    ref[:, :K] = (img.float().reshape(B, 3, gg, P, gg, P).permute(0, 2, 4, 1, 3, 5)
+                  .reshape(B * gg * gg, K).to(tdt))
+    outs = []
+    for variant in (0, 1):
+        # NaN-filled (pad columns must be written) with a canary row past the end
+        buf = torch.full((B * gg * gg + 1, Kp), float("nan"), device="cuda", dtype=tdt)
+        _check(lib, lib.miclip_op_im2col(code, icode, img.data_ptr(), buf.data_ptr(), B, R, P, Kp,
+                                         variant, _stream()))
+        torch.cuda.synchronize()
+        assert torch.isnan(buf[-1].float()).all(), "wrote past the end"
+        outs.append(buf[:-1])
+    assert torch.equal(outs[0].view(torch.int16), ref.view(torch.int16))
+    assert torch.equal(outs[1].view(torch.int16), ref.view(torch.int16))
+    # refusals: bad variant, Kp below 3*P*P, R not a multiple of P
+    assert lib.miclip_op_im2col(code, icode, img.data_ptr(), outs[0].data_ptr(), B, R, P, Kp, 2,
+                                _stream()) != 0
+    assert lib.miclip_op_im2col(code, icode, img.data_ptr(), outs[0].data_ptr(), B, R, P, K - 1, 0,
+                                _stream()) != 0
+    assert lib.miclip_op_im2col(code, icode, img.data_ptr(), outs[0].data_ptr(), B, R + 1, P, Kp, 0,
+                                _stream()) != 0
