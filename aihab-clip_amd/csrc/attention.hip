@@ -512,11 +512,27 @@ __global__ __launch_bounds__(NWMAX * 64) void attention_kernel(
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const float c2 = qk_scale * kLog2e;
+  // A last key tile holding 1-3 keys (N = 32k + 1..3, e.g. ViT-L/14@336's 577) is
+  // not run as a 29/32-to-31/32-masked MFMA tile: its keys go through
+  // attend_extra_keys on VALU (as the x8 kernel's key 256), 1/19 of the key loop
+  // at N = 577. Same staging swizzles (DH = 64).
+  const int nfull = N >> 5, nextra = N - 32 * nfull;
+  const bool xkeys = DH == 64 && !CAUSAL && nextra > 0 && nextra <= 3 && nfull >= 2;
   for (int chunk = wave; chunk < nchunks; chunk += nw) {
     i16x8 qf[G::NKS];
     load_q<T, DH>(qf, base, ld, chunk, N, lane);
     f32x16 o[G::NDT];
     float lsum, m;
+    if constexpr (DH == 64 && !CAUSAL) {
+      if (xkeys) {
+        attend_chunk<T, CAUSAL, DH>(kimg, vimg, qf, chunk, N, Npad, c2, lane, o, lsum, m, 0,
+                                    nfull, prio, true, false);
+        attend_extra_keys<T>(kimg, vimg, qf, o, lsum, m, 32 * nfull, nextra, c2, lane);
+        lsum = xor32_sum(lsum);
+        attend_store<T, DH>(o, lsum, chunk, N, out + (size_t)b * N * D + h * DH, D, lane);
+        continue;
+      }
+    }
     attend_chunk<T, CAUSAL, DH>(kimg, vimg, qf, chunk, N, Npad, c2, lane, o, lsum, m, 0, -1,
                                 prio);
     attend_store<T, DH>(o, lsum, chunk, N, out + (size_t)b * N * D + h * DH, D, lane);
@@ -1305,10 +1321,15 @@ hipError_t attn_launch_plain(const void* qkv, void* out, int B, int N, int H, hi
   // 10 waves put 6 chunks on one SIMD (waves 0, 4, 8), 12 or 16 waves at most 5 --
   // 0.312-0.322 (10) -> 0.287-0.303 (12) / 0.284-0.296 ms (16) per B = 128 launch,
   // bit-identical (scripts/probe/attn_waves.py, profiles/r04/configs/attn577_waves.jsonl).
-  // `waves` (variants 10-16) forces a count for that probe.
+  // `waves` (variants 10-16) forces a count for that probe. With the extra keys on
+  // VALU (N = 32k + 1..3, non-causal) the 16-wave build spills (6 VGPRs at its 128 cap)
+  // and 12 waves win: N = 577, B = 256: 0.569-0.575 (12) vs 0.592-0.595 ms (16),
+  // 0.590-0.596 before the change (profiles/r05/attn577/ab.txt).
   int nw;
   if constexpr (DH == 64) {
-    nw = nchunks < 16 ? nchunks : 16;
+    const int xk = N & 31;
+    const int cap = (!CAUSAL && xk >= 1 && xk <= 3 && N >= 64) ? 12 : 16;
+    nw = nchunks < cap ? nchunks : cap;
     if (waves > 0) {
       if (waves > 16) return hipErrorInvalidValue;
       nw = waves < nchunks ? waves : nchunks;
