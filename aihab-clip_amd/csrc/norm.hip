@@ -299,11 +299,14 @@ __global__ __launch_bounds__(256) void ln_fold_kernel(const T* __restrict__ W,
 // Rows per workgroup: 32 (gamma / beta staged once for 32 rows) while that still
 // gives every CU a few workgroups; 8 for smaller launches, where 32-row workgroups
 // leave ~6 waves per CU and the row loads' latency shows (ViT-B/32 bs=256: 12 800
-// rows = 400 workgroups of 32). The arithmetic per row is the same.
+// rows = 400 workgroups of 32), and 8 for the MX-fp8 output at any size (its
+// quantisation math leaves 5 waves per SIMD at 32 rows; C5's 131 584 x 1280 launch:
+// 0.098-0.099 vs 0.111 ms, 8 / 16 / 32 rows, 3 interleaved rounds,
+// profiles/r05/ln_mx_rows/). The arithmetic per row is the same.
 template <typename T, bool MX = false>
 hipError_t ln_h2_dispatch(const _Float16* in, const float* g, const float* b, void* out, int R,
                           int D, hipStream_t s, void* oq = nullptr, void* os = nullptr) {
-  const bool small = (R + kLnRows - 1) / kLnRows < 1024;
+  const bool small = MX || (R + kLnRows - 1) / kLnRows < 1024;
   const dim3 grid(small ? (R + 7) / 8 : (R + kLnRows - 1) / kLnRows), block(256);
 #define MICLIP_LNH_CASE(V)                                                                      \
   case V:                                                                                       \
