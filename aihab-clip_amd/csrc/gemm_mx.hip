@@ -916,16 +916,16 @@ __global__ __launch_bounds__(256) void quant_mx_kernel(const TI* __restrict__ in
 }
 
 // fp16 rows -> MX-fp8, 16-B loads: a lane takes 8 consecutive k, a 32-block is a
-// quad (max by two DPP steps), each thread 2 chunks. R * K / 8 is a multiple of 4,
-// so a quad is either wholly in range or wholly past the end.
+// quad (max by two DPP steps), one chunk per thread (2 per thread: 0.107 vs 0.103 ms
+// at C5's 131 584 x 1280, 4: 0.112; profiles/r05/quant_mx/). R * K / 8 is a multiple
+// of 4, so a quad is either wholly in range or wholly past the end.
 __global__ __launch_bounds__(256) void quant_mx_h8_kernel(const _Float16* __restrict__ in,
                                                           size_t chunks, int K,
                                                           uint8_t* __restrict__ q,
                                                           uint8_t* __restrict__ sc) {
   const int kc = K / 8;
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const size_t c = ((size_t)blockIdx.x * 2 + u) * 256 + threadIdx.x;
+  {
+    const size_t c = (size_t)blockIdx.x * 256 + threadIdx.x;
     const bool valid = c < chunks;
     const i16x8 h = *(const i16x8*)(in + (valid ? c : 0) * 8);
     float y[8];
@@ -943,8 +943,10 @@ __global__ __launch_bounds__(256) void quant_mx_h8_kernel(const _Float16* __rest
     if (valid) {
       *(uint2*)(q + c * 8) = make_uint2(lo, hi);
       if ((threadIdx.x & 3) == 0) {
-        const int r = (int)(c / kc), k = (int)(c - (size_t)r * kc) * 8;
-        sc[mx_scale_index(r, k >> 5, K / 128)] = (uint8_t)(ex + 127);
+        // 32-bit index math (chunks < 2^31, checked by the launcher)
+        const unsigned cu = (unsigned)c, r = cu / (unsigned)kc;
+        const int k = (int)(cu - r * (unsigned)kc) * 8;
+        sc[mx_scale_index((int)r, k >> 5, K / 128)] = (uint8_t)(ex + 127);
       }
     }
   }
@@ -997,7 +999,8 @@ hipError_t quant_mx(int in_f16, const void* in, int R, int K, void* q, void* sc,
   // older 8-lane-block kernel (op level only: the byte-identity test)
   if (in_f16 == 1) {
     const size_t chunks = (size_t)R * (K / 8);
-    hipLaunchKernelGGL(quant_mx_h8_kernel, dim3((unsigned)((chunks + 511) / 512)), dim3(256), 0, s,
+    if (chunks >= ((size_t)1 << 31)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(quant_mx_h8_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, s,
                        (const _Float16*)in, chunks, K, (uint8_t*)q, (uint8_t*)sc);
   } else if (in_f16)
     hipLaunchKernelGGL(quant_mx_kernel<_Float16>, dim3((segs + 3) / 4), dim3(256), 0, s,

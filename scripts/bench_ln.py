@@ -56,6 +56,17 @@ def main():
             by = R * D * 4
         ms = timeit(fn)
         print(json.dumps(dict(lib=tag, op=name, R=R, D=D, ms=round(ms, 4), gbs=round(by / ms / 1e6, 1))), flush=True)
+    # the attention output's MX quantisation before C5's out-projection (quant_mx, fp16 in)
+    R, D = 512 * 257, 1280
+    x = torch.randn(R, D, device="cuda", generator=g).half()
+    q = torch.empty(R, D, device="cuda", dtype=torch.uint8)
+    sc = torch.empty(int(lib.miclip_mx_scale_bytes(R, D)), device="cuda", dtype=torch.uint8)
+
+    def fq():
+        assert lib.miclip_op_quant_mx(x.data_ptr(), 1, R, D, q.data_ptr(), sc.data_ptr(), s) == 0
+    ms = timeit(fq)
+    print(json.dumps(dict(lib=tag, op="quant_c5", R=R, D=D, ms=round(ms, 4), gbs=round(R * D * 3 / ms / 1e6, 1))),
+          flush=True)
 
 
 if __name__ == "__main__":
