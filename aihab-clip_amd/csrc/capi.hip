@@ -836,11 +836,13 @@ int miclip_reserve(miclip_model* m, int32_t max_images, int32_t max_prompts) {
 }
 
 // Parts the batch of B images (N tokens each) is split into over streams: at
-// most m->splits, no part below 16 images, and none below kSplitRows rows -- a
-// part must keep its GEMMs above about one round of 256x256 tiles (ViT-B/32
-// bs=256, 12 800 rows: 71.0k img/s unsplit vs 64.8k split in two, same process).
+// most m->splits, no part below 16 images, and none below kSplitRows rows. Two
+// streams pay wherever the parts keep 16+ images (same-process splits A/B, round
+// 6, profiles/r06/splits/): ViT-L/14 at 32 / 64 / 96 images +5.9 / +3.1 / +8.8 %,
+// 48 and 128 level, ViT-B/32 bf16 at 256 level (86.5k vs 86.0k img/s; it lost 9 %
+// in round 1, before the 192-row tiles); three streams lose 5-15 %.
 static int image_splits(const miclip_model* m, int B, int N) {
-  constexpr int64_t kSplitRows = 16384;
+  constexpr int64_t kSplitRows = 4096;
   int splits = m->profiling ? 1 : m->splits;
   while (splits > 1 && (B < 16 * splits || (int64_t)B * N < kSplitRows * splits)) --splits;
   return splits;

@@ -891,6 +891,7 @@ MICLIP_DEV void wait_vmcnt_tile(int n) {
     case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
     case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
     case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
     case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
@@ -910,10 +911,13 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
   // lane's accumulator holds 4 consecutive output columns of one output row
   constexpr bool TR = TRQ && TrAcc<Epi>::value;
   // RB = 16-row blocks per wave quadrant: 4 -> 256-row tiles (the default), 3 ->
-  // 192-row tiles (transposed-accumulator epilogues only; the launcher picks them
-  // where a launch of 256-row tiles would leave CUs idle, e.g. ViT-B/32's N = 768
-  // GEMMs at M = 12 800). Same MFMA chains and epilogue arithmetic per element.
-  static_assert(RB == 4 || (RB == 3 && TR && DIAG == 0), "192-row tiles: TR epilogues only");
+  // 192-row, 2 -> 128-row tiles (transposed-accumulator epilogues only; the
+  // launcher picks them where 256-row tiles would leave CUs idle, e.g. ViT-B/32's
+  // N = 768 GEMMs at M = 12 800, ViT-L/14's N = 1024 ones at 32-64 images). Same
+  // MFMA chains and epilogue arithmetic per element: a row's result does not
+  // depend on the tile height.
+  static_assert(RB == 4 || ((RB == 3 || RB == 2) && TR && DIAG == 0),
+                "192- / 128-row tiles: TR epilogues only");
   constexpr int QR = RB * 16;            // rows of one wave quadrant
   constexpr int SR = 2 * QR;             // rows of one A half-tile slot (both wave rows)
   constexpr int TM = 2 * SR;             // tile rows
@@ -946,10 +950,13 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
   const int ec = (tid & 63) * 4;
 
   // A pieces of a slot: RB 4: 16 = 2 per wave (pieces 2w, 2w+1); RB 3: 12 = wave w's
-  // piece w and, for waves 0-3 (wave row 0), piece w + 8 -- so a wave's op count per
-  // A stage is a function of its wave row (2 or 1), which the counted waits use
+  // piece w and, for waves 0-3 (wave row 0), piece w + 8; RB 2: 8 = piece w -- so a
+  // wave's op count per A stage is a function of its wave row (2 or 1), which the
+  // counted waits use (APW0 / APW1: A ops per stage of wave rows 0 / 1)
   auto apiece = [&](int pp) { return RB == 4 ? wave * 2 + pp : wave + 8 * pp; };
-  auto ahas = [&](int pp) { return RB == 4 || pp == 0 || wave < 4; };   // wave-uniform
+  auto ahas = [&](int pp) { return RB == 4 || pp == 0 || (RB == 3 && wave < 4); };   // wave-uniform
+  constexpr int APW0 = RB == 2 ? 1 : 2, APW1 = RB == 4 ? 2 : 1;
+  const int apw = wr == 0 ? APW0 : APW1;   // wave-uniform
   // LDS-DMA sources of tile `id` (slot row sr = piece*8 + (lane>>3))
   auto sources = [&](int id, int& m0_, int& n0_, const T* (&as)[2][2], const T* (&bs)[2][2]) {
     int tm_, tn_;
@@ -1114,15 +1121,15 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
       stage(2, 0);
       stage(0, 1);
       stage(3, 1);
-      if (RB == 4 || wr == 0)
+      if (apw == 2)
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else   // RB 3, wave row 1: one A piece per stage
+      else   // one A piece per stage (RB 3 wave row 1, RB 2)
         asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     } else {
       // K-tile 0 was prefetched during the previous epilogue
       stage(0, 1);
       stage(3, 1);
-      wait_vmcnt_tile((RB == 4 || wr == 0 ? 4 : 3) + prev_stores);
+      wait_vmcnt_tile(2 + apw + prev_stores);
     }
     lds_barrier();
     if (wr == 1) lds_barrier();   // stagger (wave-uniform)
@@ -1143,16 +1150,19 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
 #endif
         if (p == 0 && wr == 0 && t > 0) {
           MICLIP_KSTAMP(1);
-          if (t + 1 < nk)
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-          else
+          if (t + 1 < nk) {
+            if constexpr (APW0 == 2)   // A0(t+1) + B1(t+1) may stay in flight
+              asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else
+              asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+          } else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           MICLIP_KSTAMP(6);
         }
         if (p == 3 && wr == 1 && t + 1 < nk) {
           MICLIP_KSTAMP(1);
           if (t + 2 < nk) {
-            if constexpr (RB == 4)   // A0(t+2) may stay in flight: 2 ops (RB 3: 1)
+            if constexpr (APW1 == 2)   // A0(t+2) may stay in flight: 2 ops (RB 3 / 2: 1)
               asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
             else
               asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
@@ -1463,7 +1473,7 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
     }
     }
     lds_barrier();                 // staging (buffer-1 half) free for the next tile
-    // RB 3: 12 rows per wave and pass instead of 16 (TR epilogues only)
+    // RB 3 / 2: 12 / 8 rows per wave and pass instead of 16 (TR epilogues only)
     prev_stores = full ? EpiStores<Epi, TR>::n * RB / 4 : 0;
     MICLIP_STAMP(3);              // epilogue
   }
@@ -1471,8 +1481,9 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
 #pragma unroll
   for (int i = 0; i < MICLIP_DIAG_STASH; ++i) asm volatile("" ::"v"(stash[i]));
 #endif
-  // the row tail on the same workgroups
-  for (int task = blockIdx.x; task < ntail; task += gridDim.x) {
+  // the row tail on the same workgroups, from the last one down (the workgroups
+  // with one tile fewer when the tiles are not a whole number of rounds)
+  for (int task = gridDim.x - 1 - blockIdx.x; task < ntail; task += gridDim.x) {
     lds_barrier();
     if (tail_wide)
       gemm_tail_wg<T, Epi, 2, 128>(A, W, M, N, K, epi, ntm * TM, task, smem);
@@ -1727,8 +1738,8 @@ struct TailPlan {
 };
 
 
-TailPlan plan_tail(int M, int N) {
-  const int ntm = (M + 255) / 256, ntn = N / 256, ncu = cu_count();
+TailPlan plan_tail(int M, int N, int TM = 256) {
+  const int ntm = (M + TM - 1) / TM, ntn = N / 256, ncu = cu_count();
   int a = ntn, b = ncu;
   while (b) {
     const int t = a % b;
@@ -1737,7 +1748,7 @@ TailPlan plan_tail(int M, int N) {
   }
   const int step = ncu / a;
   const int ntm_dp = ntm / step * step;
-  const int rows = M - ntm_dp * 256;
+  const int rows = M - ntm_dp * TM;
   if (ntm_dp == 0 || rows <= 0 || rows > 256 || N % 64) return TailPlan{ntm, 0, 0};
   // gemm_tail_wg tasks: 32 x 128 or 16 x 64, whichever ends sooner: the tail
   // adds (tasks per workgroup) x (task time) to the launch, and a wide task
@@ -1750,6 +1761,30 @@ TailPlan plan_tail(int M, int N) {
   const int narrow_cost = (narrow_tasks + ncu - 1) / ncu * 2;
   if (N % 128 == 0 && wide_cost < narrow_cost) return TailPlan{ntm_dp, wide_tasks, 1};
   return TailPlan{ntm_dp, narrow_tasks, 0};
+}
+
+// Row plan of the persistent kernel: where a launch of 256-row tiles is a single
+// partial round, the smallest tile height whose tiles still fit one round -- 128
+// rows, else 192 -- otherwise 256-row tiles with the row tail (plan_tail). Every
+// plan gives each row the same MFMA k order and epilogue functor, so the choice (a
+// function of M) never changes a result bit. Measured op-level, interleaved rounds
+// (profiles/r06/rows/rows_ops.jsonl): a 128- / 192-row tile costs 0.69-0.81 / 0.84-0.90
+// of a 256-row one (its DMA pieces per K-tile shrink to 3/4 / 7/8, not 1/2 / 3/4),
+// so splitting into two rounds or adding tail tasks to one round of smaller tiles
+// never paid (ViT-L/14 at 32 images, out-proj: 192-row 0.0255 ms, 128-row + tail
+// 0.0294, two rounds of 128-row 0.0378, 256-row 0.0284).
+struct RowPlan {
+  int rb;
+  TailPlan tp;
+};
+
+RowPlan choose_rows(int M, int N) {
+  const int ncu = cu_count(), ntn = N / 256;
+  if (((M + 255) / 256) * ntn <= ncu) {
+    if (((M + 127) / 128) * ntn <= ncu) return RowPlan{2, TailPlan{(M + 127) / 128, 0, 0}};
+    if (((M + 191) / 192) * ntn <= ncu) return RowPlan{3, TailPlan{(M + 191) / 192, 0, 0}};
+  }
+  return RowPlan{4, plan_tail(M, N, 256)};
 }
 
 bool gemm_shape_ok(int M, int N, int K) {
@@ -1781,7 +1816,8 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   variant %= 1000;
   const bool env_variant = false;   // an explicit variant never falls back silently
   if (variant != 0 && variant != 128 && variant != 256 && variant != 257 && variant != 258 &&
-      variant != 259 && variant != 260 && variant != 3 && variant != 192)
+      variant != 259 && variant != 260 && variant != 3 && variant != 192 && variant != 129 &&
+      variant != 130)
     return hipErrorInvalidValue;
   // default for full-size problems: the persistent staggered kernel (variant
   // 259; same-process A/B vs 258 on the ViT-L/14 shapes: QKV +1 %, out-proj +9 %,
@@ -1792,30 +1828,52 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   if (variant == 0 && !IsPatch<Epi>::value && N % 256 == 0 && K >= 128 &&
       2 * ((M + 255) / 256) * (N / 256) >= cu_count())
     variant = 259;
-  // 192-row tiles (gemm256s_kernel RB 3, transposed-accumulator epilogues): where a
-  // launch of 256-row tiles is a single partial round and 192-row tiles still fit
-  // one round, every CU that works does 3/4 of a tile's MFMAs and epilogue bytes
-  // (ViT-B/32 bs=256 out-proj / c_proj: 150 -> 201 tiles on 256 CUs). Variant 192
-  // forces them (tests, A/B).
+  // Smaller row tiles (gemm256s_kernel RB 3 / 2, transposed-accumulator epilogues)
+  // where 256-row tiles leave CUs idle for part of the launch (choose_rows; e.g.
+  // ViT-B/32 bs=256 out-proj / c_proj: 150 -> 201 tiles of 192 rows on 256 CUs;
+  // ViT-L/14 at 32 images, M = 8224, N = 1024: 132 tiles of 256 rows -> 256 of 128
+  // plus the 32-row tail). The persistent kernel also takes launches below half a
+  // round of 256-row tiles when 128-row tiles fill one (at 16 images). Variants 192
+  // / 129 / 130 force 192-row tiles / 128-row tiles / 128-row tiles + row tail.
   if constexpr (TrAcc<Epi>::value && !IsPatch<Epi>::value) {
-    if ((variant == 259 || variant == 192) && N % 256 == 0 && K >= 128 && !variant_tracc_off &&
-        !diag) {
-      const int ncu = cu_count(), ntm3 = (M + 191) / 192, t192 = ntm3 * (N / 256);
-      const int t256 = ((M + 255) / 256) * (N / 256);
-      if (variant == 192 || (by_size && t256 <= ncu && t192 <= ncu)) {
-        hipLaunchKernelGGL((gemm256s_kernel<T, Epi, true, 0, 3>), dim3(t192 < ncu ? t192 : ncu),
-                           dim3(512), 0, s, (const T*)A, (const T*)W, M, N, K, epi, gm, ntm3, 0,
-                           0);
+    const bool small_ok = by_size && N % 256 == 0 && K >= 128 &&
+                          2 * ((M + 127) / 128) * (N / 256) >= cu_count();
+    if ((variant == 259 || variant == 192 || variant == 129 || variant == 130 || small_ok) &&
+        N % 256 == 0 && K >= 128 && !variant_tracc_off && !diag) {
+      RowPlan rp{4, TailPlan{}};
+      if (variant == 192)
+        rp = RowPlan{3, TailPlan{(M + 191) / 192, 0, 0}};
+      else if (variant == 129)
+        rp = RowPlan{2, TailPlan{(M + 127) / 128, 0, 0}};
+      else if (variant == 130)
+        rp = RowPlan{2, plan_tail(M, N, 128)};
+      else if (by_size)
+        rp = choose_rows(M, N);
+      if (rp.rb != 4) {
+        const int ndp = rp.tp.ntm_dp * (N / 256), ncu = cu_count();
+        const int want = ndp > rp.tp.wgs ? ndp : rp.tp.wgs;
+        const dim3 grid(want < ncu ? want : ncu);
+        if (rp.rb == 3)
+          hipLaunchKernelGGL((gemm256s_kernel<T, Epi, true, 0, 3>), grid, dim3(512), 0, s,
+                             (const T*)A, (const T*)W, M, N, K, epi, gm, rp.tp.ntm_dp, rp.tp.wgs,
+                             rp.tp.wide & 1);
+        else
+          hipLaunchKernelGGL((gemm256s_kernel<T, Epi, true, 0, 2>), grid, dim3(512), 0, s,
+                             (const T*)A, (const T*)W, M, N, K, epi, gm, rp.tp.ntm_dp, rp.tp.wgs,
+                             rp.tp.wide & 1);
         return hipGetLastError();
       }
+      if (small_ok && variant == 0) variant = 259;   // 256-row tiles won: persistent kernel
     }
   }
-  if (variant == 192) return hipErrorInvalidValue;   // not a transposed-accumulator epilogue
+  if (variant == 192 || variant == 129 || variant == 130)
+    return hipErrorInvalidValue;   // not a transposed-accumulator epilogue
   if (variant == 259 && !IsPatch<Epi>::value && N % 256 == 0 && K >= 128) {
     // persistent staggered kernel, LDS-staged epilogue + next-tile prefetch
     const TailPlan tp = notail ? TailPlan{(M + 255) / 256, 0, 0} : plan_tail(M, N);
     const int ndp = tp.ntm_dp * (N / 256), ncu = cu_count();
-    const int grid = ndp < ncu ? ndp : ncu;
+    const int want = ndp > tp.wgs ? ndp : tp.wgs;
+    const int grid = want < ncu ? want : ncu;
     if constexpr (TrAcc<Epi>::value) {
       if (variant_tracc_off) {
         hipLaunchKernelGGL((gemm256s_kernel<T, Epi, false>), dim3(grid), dim3(512), 0, s,

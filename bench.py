@@ -12,8 +12,10 @@ driver does (ShardedBatchLoader + gather_shards):
        aihab_utils/feature_cache.py:144-162)
     -> zero-shot logits of the gathered rows (x @ visual.proj -> normalise
        -> 100 * f @ text_weights -> top-1; methods/ProLIP.py:288-293).
---scaling weak (default): 256 images per GPU, global batch 256 N.
---scaling strong: global batch 256 split 256/N per GPU.
+--scaling strong (default): global batch 256 split 256/N per GPU
+(256/128/64/32 images per rank at N = 1/2/4/8); at N > 1 the line also carries
+the weak-scaling figure (256 images per GPU) timed in the same run.
+--scaling weak: 256 images per GPU, global batch 256 N.
 `value` = global images per step * K / max-over-ranks wall time of the K steps.
 
 `python bench.py --gpus N` starts the N ranks itself (one process per GPU,
@@ -58,7 +60,9 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"])
+    ap.add_argument("--no-weak", action="store_true",
+                    help="N > 1 strong runs: skip the secondary weak-scaling measurement")
     ap.add_argument("--model", default="ViT-L/14")
     ap.add_argument("--batch", type=int, default=256,
                     help="images per GPU (weak) or global images (strong) per step")
@@ -200,6 +204,8 @@ class ClockProbe:
     delta(memtime) / delta(realtime) x 100 MHz, median over the XCDs."""
 
     NWG = 64          # 8 per XCD under round-robin dispatch
+    MIN_WINDOW_S = 0.1
+    GHZ_RANGE = (1.0, 2.4)   # MI355X core clock floor under load .. nameplate maximum
 
     def __init__(self, dev):
         import torch
@@ -226,10 +232,16 @@ class ClockProbe:
             dr = float(np.median(a1[:, 2]) - np.median(a0[:, 2]))
             if dr > 0:
                 per_xcd[int(x)] = dt / dr * 0.1        # GHz (realtime ticks at 100 MHz)
-        if not per_xcd:
-            return None, {}
-        vals = sorted(per_xcd.values())
-        return round(float(np.median(vals)), 4), {k: round(v, 4) for k, v in sorted(per_xcd.items())}
+        # a physically impossible reading (CU counter offsets across the window)
+        # is reported as rejected, never folded into the median
+        lo, hi = self.GHZ_RANGE
+        ok = {k: v for k, v in per_xcd.items() if lo <= v <= hi}
+        rej = {k: round(v, 4) for k, v in sorted(per_xcd.items()) if k not in ok}
+        if not ok:
+            return None, {}, rej
+        vals = sorted(ok.values())
+        return (round(float(np.median(vals)), 4), {k: round(v, 4) for k, v in sorted(ok.items())},
+                rej)
 
 
 def run(args, backend="nccl", load_model=None):
@@ -286,11 +298,11 @@ def run(args, backend="nccl", load_model=None):
     mean = torch.tensor(CLIP_MEAN, device=dev).view(1, 3, 1, 1)
     std = torch.tensor(CLIP_STD, device=dev).view(1, 3, 1, 1)
 
-    def make_images(a, b):
+    def make_images(a, b, n_all=n_global):
         out = torch.empty(max(b - a, 0), 3, R, R, device=dev)
         for c in range(a // 256, (b + 255) // 256):
             g = torch.Generator(device=dev).manual_seed(1234 + c)
-            u = torch.rand(min(256, n_global - 256 * c), 3, R, R, device=dev, generator=g)
+            u = torch.rand(min(256, n_all - 256 * c), 3, R, R, device=dev, generator=g)
             s0, s1 = max(a, 256 * c), min(b, 256 * c + u.shape[0])
             out[s0 - a:s1 - a] = (u[s0 - 256 * c:s1 - 256 * c] - mean) / std
         return out
@@ -310,11 +322,13 @@ def run(args, backend="nccl", load_model=None):
     _, temb = model.encode_text(toks.to(dev))
     tw = torch.nn.functional.normalize(temb, dim=-1).t().contiguous()      # [E, C]
 
-    def make_step(m):
+    def make_step(m, imgs=imgs, counts=counts):
+        has = imgs.shape[0] > 0
+
         def step():
             # this rank's slice, then the RCCL all-gather of the L2-normalised rows
             # back into the global order (gather_shards), then the zero-shot head
-            local = m.encode_image(imgs, normalize=True) if hi > lo else None
+            local = m.encode_image(imgs, normalize=True) if has else None
             feats = gather_shards(local, width=W, counts=counts)   # [n_global, W]
             return m.zero_shot(feats, tw, 100.0, k=1, apply_proj=True)
         return step
@@ -342,6 +356,15 @@ def run(args, backend="nccl", load_model=None):
             dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
         return float(dt_t.item())
 
+    def clock_window(fn, per_step_s):
+        """A clock reading over >= ClockProbe.MIN_WINDOW_S of back-to-back steps
+        (untimed): the probe's per-XCD deltas come from different CUs before and
+        after, so a short window magnifies their counter offsets."""
+        n = max(1, int(ClockProbe.MIN_WINDOW_S / max(per_step_s, 1e-6)) + 1)
+        c = ClockProbe(dev)
+        timed(fn, n, c)
+        return c, n
+
     # correctness guard on the timed path: the first 4 rows of every rank's slice,
     # gathered, are the single-GPU encode of those images in global order
     if world > 1:
@@ -359,7 +382,29 @@ def run(args, backend="nccl", load_model=None):
     clock = ClockProbe(dev) if on_gpu else None
     dt = timed(step, args.steps, clock)
     value = n_global * args.steps / dt
-    clock_ghz, clock_xcd = clock.ghz() if clock is not None else (None, {})
+    clock_steps = args.steps
+    if clock is not None and dt < ClockProbe.MIN_WINDOW_S:
+        # the timed region is too short for the probe: read the clock over a
+        # longer run of the same step right after it
+        clock, clock_steps = clock_window(step, dt / args.steps)
+    clock_ghz, clock_xcd, clock_rej = clock.ghz() if clock is not None else (None, {}, {})
+
+    weak = None
+    if args.scaling == "strong" and world > 1 and not args.no_weak:
+        # the weak-scaling figure of the same run: --batch (256) images per GPU
+        n_w = args.batch * world
+        wlo, whi = shard_range(n_w, rank, world)
+        model.reserve(whi - wlo, args.classes)
+        wstep = make_step(model, make_images(wlo, whi, n_w),
+                          [b - a for a, b in (shard_range(n_w, r, world) for r in range(world))])
+        for _ in range(max(args.warmup, 1)):
+            wstep()
+        wsteps = max(3, args.steps * (hi - lo) // 256)
+        wdt = timed(wstep, wsteps)
+        weak = {"value": round(n_w * wsteps / wdt, 2), "images_per_gpu": whi - wlo,
+                "global_batch": n_w, "steps": wsteps, "ms_per_step": round(wdt / wsteps * 1e3, 3),
+                "path_mfma_frac": None}
+        del wstep
     gf = algorithmic_gflop_per_image(cfg)
     cls_last = model.numerics()["cls_last"]
     gf_exec = executed_gflop_per_image(cfg, cls_last=cls_last)
@@ -451,8 +496,13 @@ def run(args, backend="nccl", load_model=None):
         # kernel's schedule from the chip's DVFS state on this box
         roofline["clock_ghz"] = clock_ghz
         roofline["clock_ghz_per_xcd"] = clock_xcd
-        roofline["clock_source"] = ("miclip_clock_probe: s_memtime / s_memrealtime per XCD, "
-                                    "before and after the timed steps on the bench stream")
+        roofline["clock_source"] = (
+            "miclip_clock_probe: s_memtime / s_memrealtime per XCD, before and after "
+            + ("the timed steps" if clock_steps == args.steps else
+               f"{clock_steps} back-to-back steps right after the timed ones (timed region "
+               f"< {ClockProbe.MIN_WINDOW_S} s)")
+            + f" on the bench stream; XCD readings outside {ClockProbe.GHZ_RANGE} GHz rejected")
+        roofline["clock_rejected_per_xcd"] = clock_rej
         roofline["frac_at_clock"] = (round(roofline["frac"] * 2.4 / clock_ghz, 4)
                                      if clock_ghz else None)
 
@@ -495,6 +545,9 @@ def run(args, backend="nccl", load_model=None):
             line["fold_ab_img_s"] = abf
         if abg:
             line["gemm_ab_img_s"] = abg
+        if weak:
+            weak["path_mfma_frac"] = round(weak["value"] * gf * 1e9 / (world * peak * 1e12), 4)
+            line["weak_scaling"] = weak
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -291,7 +291,10 @@ int miclip_profile_read(miclip_model* m, miclip_kernel_stat* out, int32_t n, int
  * epi 2: C fp32 = . ; epi 3: no output (diagnostic: prices the epilogue);
  * epi 4: C fp16 += . (fp16 residual stream; dtype MICLIP_FP16 only).
  * N % 128 == 0 and K % 64 == 0 required. variant: 0 = tile
- * chosen by size, 128 / 256 = force the 128x128 / 256x256 kernel (N % 256 for 256).
+ * chosen by size, 128 / 256 = force the 128x128 / 256x256 kernel (N % 256 for 256);
+ * 259 = the persistent 256-row-tile kernel; 192 / 129 / 130 = its 192-row tiles /
+ * 128-row tiles / 128-row tiles + row tail (epi 0 and 4 only; N % 256, K >= 128).
+ * 259 / 192 / 129 / 130 give bit-identical results (same k order and epilogue per row).
  * Replaces torch Linear (clip/model.py:171-175) and MHA in/out projections. */
 int miclip_op_gemm(int32_t dtype, const void* A, const void* W, const float* bias, void* C,
                    int32_t M, int32_t N, int32_t K, int32_t epi, int32_t act, int32_t variant,

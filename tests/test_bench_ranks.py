@@ -71,20 +71,22 @@ ARGV = ["--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "4", "--model
         "--classes", "5", "--no-profile", "--no-cpu-baseline"]
 
 
-def _rank(rank, world, port, q):
+def _rank(rank, world, port, q, extra):
     import torch.distributed as dist
     import bench
     os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    line = bench.run(bench.parse(ARGV), backend="gloo", load_model=_stub_loader)
+    line = bench.run(bench.parse(ARGV + extra), backend="gloo", load_model=_stub_loader)
     q.put((rank, line, dist.is_initialized()))
 
 
-def test_bench_rank_logic_world2_gloo():
+@pytest.mark.parametrize("scaling", ["strong", "weak"])
+def test_bench_rank_logic_world2_gloo(scaling):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     world, port = 2, _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    extra = [] if scaling == "strong" else ["--scaling", "weak"]     # strong is the default
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q, extra)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -98,9 +100,16 @@ def test_bench_rank_logic_world2_gloo():
     line1, still1 = res[1]
     assert line1 is None and not still0 and not still1     # rank 0 reports; groups torn down
     assert line0["n_gpus"] == 2 and line0["steps"] == 2 and line0["warmup"] == 1
-    assert line0["config"]["global_batch"] == 8 and line0["config"]["images_per_gpu"] == 4
-    assert line0["scaling"] == "weak" and line0["value"] > 0
-    assert line0["value"] == pytest.approx(8 * 2 / (line0["ms_per_step"] * 2 / 1e3), rel=1e-2)
+    assert line0["scaling"] == scaling and line0["value"] > 0
+    if scaling == "weak":     # --batch images per GPU
+        assert line0["config"]["global_batch"] == 8 and line0["config"]["images_per_gpu"] == 4
+        assert "weak_scaling" not in line0
+    else:                     # the global --batch split over the ranks
+        assert line0["config"]["global_batch"] == 4 and line0["config"]["images_per_gpu"] == 2
+        w = line0["weak_scaling"]             # plus the weak figure of the same run
+        assert w["global_batch"] == 8 and w["images_per_gpu"] == 4 and w["value"] > 0
+    n = line0["config"]["global_batch"]
+    assert line0["value"] == pytest.approx(n * 2 / (line0["ms_per_step"] * 2 / 1e3), rel=1e-2)
     assert line0["clock_ghz"] is None and line0["roofline"] is None     # no HIP device here
 
 

@@ -7,7 +7,7 @@ stream split and the last row, so the production launch shapes meet the
 reference (as tests/test_gpu_lnfold.py:test_benched_config_vitl14_bs256 does
 for C3):
 
-  C2  ViT-B/32 bf16, bs=256: M = 12 800 unsplit (N = 768 tile columns)
+  C2  ViT-B/32 bf16, bs=256: 2 streams of M = 6 400 (N = 768 tile columns)
   C4  ViT-L/14@336px fp16, bs=256: 2 streams of M = 73 856, attention at
       N = 577 (one head per workgroup), row tails
   C5  ViT-H-14 mxfp8, bs=512: MX-fp8 GEMMs over 2 streams of M = 65 792,
@@ -45,7 +45,7 @@ def _needs_gpu():
 
 
 @pytest.mark.parametrize("tag,name,dtype,bs,splits,tol,ctol", [
-    ("vitb32", "ViT-B/32", "bf16", 256, 1, 1e-3, 1e-3),
+    ("vitb32", "ViT-B/32", "bf16", 256, 2, 1e-3, 1e-3),
     ("vitl14_336", "ViT-L/14@336px", "fp16", 256, 2, 1e-3, 1e-3),
     ("vith14", "ViT-H-14", "mxfp8", 512, 2, 2e-3, 1e-2),
 ])
@@ -82,4 +82,25 @@ def test_large_batch_config(golden, tag, name, dtype, bs, splits, tol, ctol):
     assert torch.equal(fh, feats), f"{(fh != feats).any(1).sum().item()} rows differ"
     again = m.encode_image(x).cpu()
     assert torch.equal(again, feats), "large-batch encode is not deterministic"
+    del m
+
+
+def test_strong_split_shards_bitwise_vitl14():
+    """SURVEY §8e's strong split: a global batch of 256 split G = 2/4/8/16 ways (128 /
+    64 / 32 / 16 images per rank: M = 32 896 .. 4 112 GEMM rows, where the launcher
+    switches to 192- / 128-row tiles and the 16-image parts to one stream) must encode each rank's
+    slice to exactly the rows of the single-GPU bs=256 encode, so the sharded
+    feature cache equals the single-GPU one bit for bit
+    (aihab_utils/feature_cache.py:114-162; clip/model.py:216-235)."""
+    import miclip
+    from miclip.weights import synthetic_images
+    _, m, _ = miclip.load("ViT-L/14", device="cuda", compute_dtype="fp16", surface="openai")
+    x = torch.from_numpy(synthetic_images(256, 224, seed=5)).cuda()
+    full = m.encode_image(x, normalize=True)
+    for G in (2, 4, 8, 16):
+        b = 256 // G
+        for r in (0, G - 1):
+            part = m.encode_image(x[r * b:(r + 1) * b], normalize=True)
+            d = part != full[r * b:(r + 1) * b]
+            assert not d.any(), f"G={G} rank {r}: {d.any(1).sum().item()} rows differ"
     del m

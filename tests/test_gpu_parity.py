@@ -159,13 +159,13 @@ def test_batch_invariance_and_shards():
     exactly the single-GPU cache."""
     from miclip.weights import synthetic_images
     m = _model("ViT-B/32", "fp16")
-    # 96 x 50 token rows: below the split threshold, one stream (the split path
-    # at the benched batch: test_gpu_lnfold.test_benched_config_vitl14_bs256)
-    assert m.image_splits(96) == 1 and m.image_splits(256) == 1
+    # two streams from 2 x 4096 token rows and 2 x 16 images (capi.hip image_splits):
+    # the 192-image batch runs split, its 32-image shards on one stream
     m.set_splits(2)
-    imgs = torch.from_numpy(synthetic_images(96, 224, seed=3)).cuda()
+    assert m.image_splits(96) == 1 and m.image_splits(192) == 2 and m.image_splits(32) == 1
+    imgs = torch.from_numpy(synthetic_images(192, 224, seed=3)).cuda()
     full = m.encode_image(imgs)
-    parts = torch.cat([m.encode_image(imgs[i:i + 32]) for i in range(0, 96, 32)])
+    parts = torch.cat([m.encode_image(imgs[i:i + 32]) for i in range(0, 192, 32)])
     assert torch.equal(full, parts)
     again = m.encode_image(imgs)
     assert torch.equal(full, again), "encode is not deterministic"
