@@ -40,26 +40,20 @@ stamps: $(OBJS)
 
 # timing diagnostics (outputs meaningless): the library without the vision-tower
 # attention / without the large ln_stats launches, to price what each costs inside
-# the two-stream step (bench.py with MICLIP_LIB=build/diag/libmiclip_<x>.so)
+# the two-stream step (bench.py with MICLIP_LIB=build/diag/libmiclip_<x>.so). The
+# product sources carry no diagnostic code: the entry point is renamed at compile
+# time and wrapped by scripts/diag/skip.hip.
 DIAG_DIR := build/diag
 diag: $(OBJS)
 	@mkdir -p $(DIAG_DIR)
-	$(HIPCC) $(HIPFLAGS) -fno-honor-nans -fno-slp-vectorize -DMICLIP_DIAG_SKIP_ATTN -c $(SRC_DIR)/attention.hip -o $(DIAG_DIR)/attention_noattn.o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(DIAG_DIR)/attention_noattn.o $(filter-out $(OBJ_DIR)/attention.o,$(OBJS)) -o $(DIAG_DIR)/libmiclip_noattn.so
-	$(HIPCC) $(HIPFLAGS) -DMICLIP_DIAG_SKIP_LNSTATS -c $(SRC_DIR)/norm.hip -o $(DIAG_DIR)/norm_nolns.o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(DIAG_DIR)/norm_nolns.o $(filter-out $(OBJ_DIR)/norm.o,$(OBJS)) -o $(DIAG_DIR)/libmiclip_nolns.so
-
-# timing diagnostic: the persistent GEMM with 16 / 32 / 64 registers held live across
-# its main loop (MICLIP_DIAG_STASH; outputs unchanged), pricing a deferred-epilogue stash
-diag-stash: $(OBJS)
-	@mkdir -p $(DIAG_DIR)
-	for n in 16 32 64; do \
-	  $(HIPCC) $(HIPFLAGS) -DMICLIP_DIAG_STASH=$$n -c $(SRC_DIR)/gemm.hip -o $(DIAG_DIR)/gemm_stash$$n.o && \
-	  $(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(DIAG_DIR)/gemm_stash$$n.o $(filter-out $(OBJ_DIR)/gemm.o,$(OBJS)) -o $(DIAG_DIR)/libmiclip_stash$$n.so || exit 1; \
-	  $(HIPCC) $(HIPFLAGS) -DMICLIP_DIAG_STASH=$$n --cuda-device-only -S $(SRC_DIR)/gemm.hip -o $(DIAG_DIR)/gemm_stash$$n.s || exit 1; \
-	done
+	$(HIPCC) $(HIPFLAGS) -fno-honor-nans -fno-slp-vectorize -Dattention=attention_product -c $(SRC_DIR)/attention.hip -o $(DIAG_DIR)/attention_renamed.o
+	$(HIPCC) $(HIPFLAGS) -DSKIP_ATTN -c scripts/diag/skip.hip -o $(DIAG_DIR)/skip_attn.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(DIAG_DIR)/attention_renamed.o $(DIAG_DIR)/skip_attn.o $(filter-out $(OBJ_DIR)/attention.o,$(OBJS)) -o $(DIAG_DIR)/libmiclip_noattn.so
+	$(HIPCC) $(HIPFLAGS) -Dln_stats=ln_stats_product -c $(SRC_DIR)/norm.hip -o $(DIAG_DIR)/norm_renamed.o
+	$(HIPCC) $(HIPFLAGS) -DSKIP_LNSTATS -c scripts/diag/skip.hip -o $(DIAG_DIR)/skip_lns.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) $(DIAG_DIR)/norm_renamed.o $(DIAG_DIR)/skip_lns.o $(filter-out $(OBJ_DIR)/norm.o,$(OBJS)) -o $(DIAG_DIR)/libmiclip_nolns.so
 
 clean:
 	rm -rf build $(LIB)
 
-.PHONY: all clean asm stamps diag diag-stash
+.PHONY: all clean asm stamps diag

@@ -1519,9 +1519,6 @@ hipError_t attention_q0(int dtype, const void* qkv, void* out, int B, int N, int
 hipError_t attention(int dtype, const void* qkv, void* out, int B, int N, int H, int causal,
                      hipStream_t s, int variant, int head_dim) {
   if (B < 1 || N < 1 || H < 1) return hipErrorInvalidValue;
-#ifdef MICLIP_DIAG_SKIP_ATTN   // timing diagnostic (make diag): no vision-tower attention
-  if (!causal && N > 200) return hipSuccess;
-#endif
   if (dtype == kF16)
     return causal ? attn_launch<_Float16, true>(qkv, out, B, N, H, head_dim, s, variant)
                   : attn_launch<_Float16, false>(qkv, out, B, N, H, head_dim, s, variant);

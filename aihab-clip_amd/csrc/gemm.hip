@@ -898,11 +898,7 @@ MICLIP_DEV void wait_vmcnt_tile(int n) {
   }
 }
 
-// DIAG (diagnostic builds of the main loop, outputs meaningless): 1 = the
-// K-tile DMAs of every odd K-tile are skipped (the loop reuses stale LDS), 2 =
-// only K-tiles 0 and 1 are fetched. Used to tell the L2->LDS path from the
-// schedule as the main loop's limit (scripts/bench_ops.py variant suffixes).
-template <typename T, class Epi, bool TRQ = true, int DIAG = 0, int RB = 4>
+template <typename T, class Epi, bool TRQ = true, int RB = 4>
 __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
                                                        const T* __restrict__ W, int M, int N,
                                                        int K, Epi epi, int gm, int ntm_dp,
@@ -916,7 +912,7 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
   // N = 768 GEMMs at M = 12 800, ViT-L/14's N = 1024 ones at 32-64 images). Same
   // MFMA chains and epilogue arithmetic per element: a row's result does not
   // depend on the tile height.
-  static_assert(RB == 4 || ((RB == 3 || RB == 2) && TR && DIAG == 0),
+  static_assert(RB == 4 || ((RB == 3 || RB == 2) && TR),
                 "192- / 128-row tiles: TR epilogues only");
   constexpr int QR = RB * 16;            // rows of one wave quadrant
   constexpr int SR = 2 * QR;             // rows of one A half-tile slot (both wave rows)
@@ -1006,12 +1002,6 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
       }
   };
   auto stage = [&](int slot_kind, int tile) {
-    if constexpr (DIAG == 1) {
-      if (tile & 1) return;
-    }
-    if constexpr (DIAG == 2) {
-      if (tile >= 2) return;
-    }
     const int buf = tile & 1, k0 = tile * 64;
     char* slot = smem + (buf * 4 + slot_kind) * HALF;
     const unsigned kb = (unsigned)k0 * (unsigned)sizeof(T);
@@ -1071,15 +1061,6 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
 
   int prev_stores = -1;   // -1: first tile (full prologue)
   int id = blockIdx.x;
-#ifdef MICLIP_DIAG_STASH
-  // timing diagnostic (make diag-stash, outputs unchanged): MICLIP_DIAG_STASH
-  // registers held live across every K-tile of the main loop, as the stash of a
-  // deferred epilogue (the next tile's K loop finishing this tile's activation
-  // and stores) would be -- prices the register budget of that design
-  float stash[MICLIP_DIAG_STASH];
-#pragma unroll
-  for (int i = 0; i < MICLIP_DIAG_STASH; ++i) asm volatile("v_mov_b32 %0, %1" : "=v"(stash[i]) : "v"(i));
-#endif
   MICLIP_STAMP_BEGIN;
   if (id < ndp) sources(id, m0, n0, asrc, bsrc);
   for (; id < ndp; id += gridDim.x) {
@@ -1142,12 +1123,6 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
       const char* sB1 = smem + (buf * 4 + 3) * HALF + boff;
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
-#ifdef MICLIP_DIAG_STASH
-        if (p == 0) {
-#pragma unroll
-          for (int i = 0; i < MICLIP_DIAG_STASH; ++i) asm volatile("" : "+v"(stash[i]));
-        }
-#endif
         if (p == 0 && wr == 0 && t > 0) {
           MICLIP_KSTAMP(1);
           if (t + 1 < nk) {
@@ -1477,10 +1452,6 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
     prev_stores = full ? EpiStores<Epi, TR>::n * RB / 4 : 0;
     MICLIP_STAMP(3);              // epilogue
   }
-#ifdef MICLIP_DIAG_STASH
-#pragma unroll
-  for (int i = 0; i < MICLIP_DIAG_STASH; ++i) asm volatile("" ::"v"(stash[i]));
-#endif
   // the row tail on the same workgroups, from the last one down (the workgroups
   // with one tile fewer when the tiles are not a whole number of rounds)
   for (int task = gridDim.x - 1 - blockIdx.x; task < ntail; task += gridDim.x) {
@@ -1722,9 +1693,6 @@ constexpr int kGemmNoTail = 1 << 16;
 constexpr int kGemmTailFirst = 1 << 17;
 // kGemmStagger: 8-us round stagger, see gemm256_kernel
 constexpr int kGemmStagger = 1 << 18;
-// kGemmDiag1 / kGemmDiag2: gemm256s_kernel DIAG 1 / 2 (diagnostic, garbage output)
-constexpr int kGemmDiag1 = 1 << 19;
-constexpr int kGemmDiag2 = 1 << 20;
 // kGemmTrAccOff: the persistent kernel's fp32 row-staging epilogue instead of the
 // transposed-accumulator one for EpiStore / EpiStoreLN (A/B)
 constexpr int kGemmTrAccOff = 1 << 21;
@@ -1808,10 +1776,8 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
   const bool notail = variant & kGemmNoTail;
   const bool tail_first = variant & kGemmTailFirst;
   const bool stagger = variant & kGemmStagger;
-  const int diag = variant & kGemmDiag1 ? 1 : variant & kGemmDiag2 ? 2 : 0;
   const bool variant_tracc_off = variant & kGemmTrAccOff;
-  variant &= ~(kGemmNoTail | kGemmTailFirst | kGemmStagger | kGemmDiag1 | kGemmDiag2 |
-               kGemmTrAccOff);
+  variant &= ~(kGemmNoTail | kGemmTailFirst | kGemmStagger | kGemmTrAccOff);
   const int gm = variant >= 1000 ? variant / 1000 : gemm_group();
   variant %= 1000;
   const bool env_variant = false;   // an explicit variant never falls back silently
@@ -1839,7 +1805,7 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
     const bool small_ok = by_size && N % 256 == 0 && K >= 128 &&
                           2 * ((M + 127) / 128) * (N / 256) >= cu_count();
     if ((variant == 259 || variant == 192 || variant == 129 || variant == 130 || small_ok) &&
-        N % 256 == 0 && K >= 128 && !variant_tracc_off && !diag) {
+        N % 256 == 0 && K >= 128 && !variant_tracc_off) {
       RowPlan rp{4, TailPlan{}};
       if (variant == 192)
         rp = RowPlan{3, TailPlan{(M + 191) / 192, 0, 0}};
@@ -1854,11 +1820,11 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
         const int want = ndp > rp.tp.wgs ? ndp : rp.tp.wgs;
         const dim3 grid(want < ncu ? want : ncu);
         if (rp.rb == 3)
-          hipLaunchKernelGGL((gemm256s_kernel<T, Epi, true, 0, 3>), grid, dim3(512), 0, s,
+          hipLaunchKernelGGL((gemm256s_kernel<T, Epi, true, 3>), grid, dim3(512), 0, s,
                              (const T*)A, (const T*)W, M, N, K, epi, gm, rp.tp.ntm_dp, rp.tp.wgs,
                              rp.tp.wide & 1);
         else
-          hipLaunchKernelGGL((gemm256s_kernel<T, Epi, true, 0, 2>), grid, dim3(512), 0, s,
+          hipLaunchKernelGGL((gemm256s_kernel<T, Epi, true, 2>), grid, dim3(512), 0, s,
                              (const T*)A, (const T*)W, M, N, K, epi, gm, rp.tp.ntm_dp, rp.tp.wgs,
                              rp.tp.wide & 1);
         return hipGetLastError();
@@ -1877,21 +1843,6 @@ hipError_t launch(const void* A, const void* W, int M, int N, int K, Epi epi, hi
     if constexpr (TrAcc<Epi>::value) {
       if (variant_tracc_off) {
         hipLaunchKernelGGL((gemm256s_kernel<T, Epi, false>), dim3(grid), dim3(512), 0, s,
-                           (const T*)A, (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs,
-                           tp.wide & 1);
-        return hipGetLastError();
-      }
-    }
-    if constexpr (std::is_same_v<Epi, EpiResidual<_Float16>> ||
-                  std::is_same_v<Epi, EpiStore<_Float16, ACT_QUICKGELU>>) {
-      if (diag == 1) {
-        hipLaunchKernelGGL((gemm256s_kernel<T, Epi, true, 1>), dim3(grid), dim3(512), 0, s,
-                           (const T*)A, (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs,
-                           tp.wide & 1);
-        return hipGetLastError();
-      }
-      if (diag == 2) {
-        hipLaunchKernelGGL((gemm256s_kernel<T, Epi, true, 2>), dim3(grid), dim3(512), 0, s,
                            (const T*)A, (const T*)W, M, N, K, epi, gm, tp.ntm_dp, tp.wgs,
                            tp.wide & 1);
         return hipGetLastError();

@@ -75,9 +75,7 @@ def main():
         # "258n": variant 258 without the row-tail split (gemm.hip kGemmNoTail)
         # "258f": tail workgroups interleaved with the first tiles (kGemmTailFirst)
         # "258s": round stagger (kGemmStagger)
-        # "259d" / "259e": diagnostic main loops (gemm256s DIAG 1 / 2: odd K-tiles not
-        # fetched / only K-tiles 0-1 fetched; garbage output, timing only)
-        suffix = {"n": 1 << 16, "f": 1 << 17, "s": 1 << 18, "d": 1 << 19, "e": 1 << 20}
+        suffix = {"n": 1 << 16, "f": 1 << 17, "s": 1 << 18}
         vlist = [int(x[:-1]) | suffix[x[-1]] if x[-1] in suffix else int(x)
                  for x in args.variants.split(",")]
         for v in vlist:

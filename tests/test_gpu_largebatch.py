@@ -14,7 +14,7 @@ for C3):
       head dim 80 (open_clip shapes; OpenAI surface: pre-projection goldens)
 
 Each golden row must be within the config's tolerance of the reference
-(1-cos <= 1e-3; MX-fp8: the stated fp8 bound 2e-3, tests/test_gpu_parity.py)
+(1-cos <= 1e-3, MX-fp8 included; its centred bound 1e-2, tests/test_gpu_parity.py)
 and bitwise equal to the small-batch encode of the same images (batch
 invariance: the GEMM tiles, tails and splits keep one k order). A half-precision
 input batch in the compute dtype (miclip_encode_image_ex) gives the same
@@ -47,7 +47,7 @@ def _needs_gpu():
 @pytest.mark.parametrize("tag,name,dtype,bs,splits,tol,ctol", [
     ("vitb32", "ViT-B/32", "bf16", 256, 2, 1e-3, 1e-3),
     ("vitl14_336", "ViT-L/14@336px", "fp16", 256, 2, 1e-3, 1e-3),
-    ("vith14", "ViT-H-14", "mxfp8", 512, 2, 2e-3, 1e-2),
+    ("vith14", "ViT-H-14", "mxfp8", 512, 2, 1e-3, 1e-2),
 ])
 def test_large_batch_config(golden, tag, name, dtype, bs, splits, tol, ctol):
     import miclip

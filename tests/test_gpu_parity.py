@@ -274,11 +274,12 @@ def test_zero_shot_head_vs_torch(B, C, k):
 
 
 # MICLIP_MXFP8: parity unpinned with respect to the
-# reference (no fp8 path there). The vision tower runs MX-fp8 GEMMs, bounded
-# against the fp32 goldens with fp8 tolerances a few times above what the
-# block-scaled e4m3 path measures (image 1-cos <= 5.5e-4); the
-# text tower runs fp16 under mxfp8 and meets the north star's 1e-3.
-MX_COS_TOL_IMAGE = 2e-3
+# reference (no fp8 path there). The vision tower runs MX-fp8 GEMMs and is held
+# to the north star's 1e-3 like every other path (measured 7.3e-4 ViT-H-14, 8.2e-4
+# ViT-B/32, profiles/r05/configs/parity.log); the centred figure -- the image-
+# specific part of the feature, which fp8 perturbs ~10x more than fp16 -- stays
+# bounded at 1e-2 and printed. The text tower runs fp16 under mxfp8.
+MX_COS_TOL_IMAGE = 1e-3
 MX_CENTRED_TOL_IMAGE = 1e-2
 MX_COS_TOL_TEXT = COS_TOL
 
