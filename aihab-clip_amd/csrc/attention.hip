@@ -1050,6 +1050,142 @@ __global__ __launch_bounds__(SPLIT ? 512 : 640) void attention_pipe_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// The x8 kernel's full query chunk: one wave's 32 queries against key tiles 0..7
+// (keys 0..255, never masked), with the softmax's VALU work moved onto the matrix
+// pipe. The kernel is VALU-bound at N = 257 (r04 PMC: 22 % MFMA busy at 17 VALU per
+// MFMA; the tile loop issued ~75 VALU + 16 v_exp per 8 MFMAs). Here:
+//  * Q arrives pre-scaled by c2 = scale * log2(e) (prescale_q: one fp32 product
+//    and one rounding per element, once per head), so S' = K . Q'^T is already in
+//    the base-2 softmax domain;
+//  * the running max leaves through the MFMA chain: each tile's S' chain starts
+//    from a fifth k-step ones . (-m~)^T (A = ones in k-slot 0 of the lanes' first
+//    8-half group, B = -m~ rounded to the compute dtype), so the accumulator holds
+//    S' - m~ and p = exp2(acc) needs no per-element FMA (m~ only has to be the same
+//    shift for every p of the row: p, l and O all use it);
+//  * the lazy-rescale test is one v_max3 tree against the threshold, per lane (the
+//    wave-wide vote covers both lane halves, no lane exchange on the fast path);
+//  * the row sum is a v_dot2 of the rounded P pairs with ones (the sum of exactly
+//    the P values the P.V MFMAs use), 8 ops instead of 16 adds;
+//  * the 8 tiles are unrolled: every LDS read is a per-lane base + an immediate.
+// Tile 0 finds the first max with the full reduction (m starts undefined).
+// Leaves the unnormalised O^T, this lane's partial row sum (reduce across the lane
+// halves after any further keys) and m~ (scaled log2 domain) for attend_extra_keys.
+// ---------------------------------------------------------------------------
+template <typename T>
+MICLIP_DEV void prescale_q(i16x8 (&qf)[4], float c2) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qf[s][j] = to_bits<T>(from_bits<T>(qf[s][j]) * c2);
+}
+
+template <typename T>
+MICLIP_DEV void attend_full_x8(const char* kimg, const char* vimg, const i16x8 (&qf)[4], int lane,
+                               f32x16 (&o)[2], float& lsum, float& m) {
+  using G = HeadGeom<64>;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+  unsigned kb = (unsigned)(uintptr_t)(const LDS_AS char*)kimg;
+  unsigned vb = (unsigned)(uintptr_t)(const LDS_AS char*)vimg;
+  asm("" : "+s"(kb), "+s"(vb));
+  const LDS_AS char* kp[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    kp[s] = (const LDS_AS char*)(uintptr_t)(kb + l32 * G::ROWB + (G::kswz(2 * s + hh, l32) << 4));
+  const LDS_AS char* vp[2];
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    const int ch = 4 * dt + 2 * (g & 1) + (tp >> 1), vr = 4 * (g >> 1) + tq;
+    vp[dt] = (const LDS_AS char*)(uintptr_t)(vb + vr * G::ROWB + (G::vswz(ch, vr) << 4) + 8 * (tp & 1));
+  }
+  // the shift k-step: A[key][k] = (k == 0), B[k][query] = -m~ (k == 0): lanes of the
+  // first half hold k-slots 0..7 (hh = 0), so only their first element is non-zero
+  const short one = to_bits<T>(1.0f);
+  const i16x8 ka = {hh == 0 ? one : (short)0, 0, 0, 0, 0, 0, 0, 0};
+  i16x8 qm = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint32_t ones2 = (uint32_t)(unsigned short)one * 0x10001u;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    o[0][r] = 0.f;
+    o[1][r] = 0.f;
+  }
+  lsum = 0.f;
+  m = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < 8; ++kt) {
+    f32x16 sacc;
+    __builtin_amdgcn_s_setprio(1);
+    if (kt == 0) {
+      const i16x8 kf = *(const LDS_AS i16x8*)(kp[0]);
+      sacc = Mfma<T>::m32(kf, qf[0], f32x16{});
+    } else {
+      const i16x8 kf = *(const LDS_AS i16x8*)(kp[0] + kt * G::TILEB);
+      sacc = Mfma<T>::m32(ka, qm, f32x16{});
+      sacc = Mfma<T>::m32(kf, qf[0], sacc);
+    }
+#pragma unroll
+    for (int s = 1; s < 4; ++s) {
+      const i16x8 kf = *(const LDS_AS i16x8*)(kp[s] + kt * G::TILEB);
+      sacc = Mfma<T>::m32(kf, qf[s], sacc);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    const float t0 = fmaxf(fmaxf(sacc[0], sacc[1]), sacc[2]);
+    const float t1 = fmaxf(fmaxf(sacc[3], sacc[4]), sacc[5]);
+    const float t2_ = fmaxf(fmaxf(sacc[6], sacc[7]), sacc[8]);
+    const float t3 = fmaxf(fmaxf(sacc[9], sacc[10]), sacc[11]);
+    const float t4 = fmaxf(fmaxf(sacc[12], sacc[13]), sacc[14]);
+    const float tmax = fmaxf(fmaxf(fmaxf(t0, t1), t2_), fmaxf(fmaxf(t3, t4), sacc[15]));
+    if (kt == 0 || !__all(tmax <= 8.0f)) {
+      // first tile, or a tile max more than 2^8 above m~: new m~ = the row max
+      // (both lane halves), rounded to the compute dtype; O and l rescaled
+      const float rmax = xor32_max(tmax) + (kt == 0 ? 0.f : m);   // absolute, scaled domain
+      const float mn = from_bits<T>(to_bits<T>(kt == 0 ? rmax : fmaxf(m, rmax)));
+      const float d = mn - m;           // kt > 0: >= 0 up to the rounding of mn
+      if (kt > 0) {
+        const float alpha = __builtin_amdgcn_exp2f(-d);
+        lsum *= alpha;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          o[0][r] *= alpha;
+          o[1][r] *= alpha;
+        }
+      }
+      const float sh = kt == 0 ? mn : d;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[r] -= sh;
+      m = mn;
+      qm[0] = hh == 0 ? to_bits<T>(-mn) : (short)0;
+    }
+    i16x8 pf[2];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sacc[r] = __builtin_amdgcn_exp2f(sacc[r]);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pf[s2][j] = to_bits<T>(sacc[8 * s2 + j]);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const u32x4 w = __builtin_bit_cast(u32x4, pf[s2]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) lsum = dot2acc<T>(w[e], ones2, lsum);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const LDS_AS char* a0 = vp[dt] + kt * G::TILEB + 16 * G::ROWB * s2;
+        const i16x4 lo = ds_read_tr16_b64(a0);
+        const i16x4 hi = ds_read_tr16_b64(a0 + 8 * G::ROWB);
+        const i16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[dt] = Mfma<T>::m32(vf, pf[s2], o[dt]);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Two workgroups per CU (variant 8, default for 8 full query chunks and at most
 // 3 more queries, N in 256..259: ViT-L/14 at 224 px). One workgroup = 8 waves (2 per
 // SIMD) walks hpw (image, head) pairs with ONE K/V buffer (Npad x 256 B, 72 KiB
@@ -1121,9 +1257,10 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
     {
       f32x16 o[2];
       float lsum, m;
-      attend_chunk<T, false, 64, false, true>(kimg, vimg, qf, wave, N, Npad, c2, lane, o, lsum, m,
-                                              0, 8, prio, true, false);
-      attend_extra_keys<T>(kimg, vimg, qf, o, lsum, m, 256, nextra, c2, lane);
+      // Q in the base-2 softmax domain: the full chunk and its extra keys take c2 = 1
+      prescale_q<T>(qf, c2);
+      attend_full_x8<T>(kimg, vimg, qf, lane, o, lsum, m);
+      attend_extra_keys<T>(kimg, vimg, qf, o, lsum, m, 256, nextra, 1.0f, lane);
       lsum = xor32_sum(lsum);
       MICLIP_STAMP(1);   // the wave's full query chunk
       attend_store<T, 64>(o, lsum, wave, N, obase, D, lane);
