@@ -405,14 +405,16 @@ static void im2col_band(const void* img, T* patches, int B, int R, int P, int Kp
                        R, P, Kp);
 }
 
-// variant 0: the band kernel where it applies (R % 4 == 0, Kp % 4 == 0: every vector
-// load and store aligned), else the per-patch kernel; 1: the per-patch kernel
+// variant 0: the band kernel where it applies (R % 4 == 0, Kp % 4 == 0 and both base
+// pointers 16-B aligned: every vector load and store aligned), else the per-patch
+// kernel (element accesses, any alignment); 1: the per-patch kernel
 template <typename T>
 static hipError_t im2col_t(int in_dtype, const void* img, T* patches, int B, int R, int P, int Kp,
                            hipStream_t s, int variant) {
   const int np = (R / P) * (R / P);
-  if (variant == 0 && R % 4 == 0 && Kp % 4 == 0 && (in_dtype == kIn32 || in_dtype == kF16 ||
-                                                    in_dtype == kBF16)) {
+  const bool aligned = ((uintptr_t)img & 15) == 0 && ((uintptr_t)patches & 15) == 0;
+  if (variant == 0 && aligned && R % 4 == 0 && Kp % 4 == 0 &&
+      (in_dtype == kIn32 || in_dtype == kF16 || in_dtype == kBF16)) {
     if (in_dtype == kIn32)
       im2col_band<T, float>(img, patches, B, R, P, Kp, s);
     else if (in_dtype == kF16)

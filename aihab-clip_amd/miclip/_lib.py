@@ -139,18 +139,26 @@ def load_library(path: str = None):
         "miclip_proto_scores": ([vp, vp, vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp],
                                 ctypes.c_int),
     }
-    # an A/B build of an older revision (MICLIP_LIB) may predate some op-level entry
-    # points: those stay unbound there; the product library must export them all
-    ab_build = "MICLIP_LIB" in os.environ
+    # an explicitly declared A/B build of an older revision (MICLIP_LIB together with
+    # MICLIP_AB_BUILD=1) may predate some op-level entry points: those stay unbound
+    # and are named on stderr; any other library -- the product one, or MICLIP_LIB
+    # alone -- must export every entry point, or loading fails here
+    ab_build = "MICLIP_LIB" in os.environ and os.environ.get("MICLIP_AB_BUILD") == "1"
+    unbound = []
     for name, (args, res) in sig.items():
         try:
             fn = getattr(lib, name)
         except AttributeError:
             if ab_build and name.startswith("miclip_op_"):
+                unbound.append(name)
                 continue
             raise
         fn.argtypes = args
         fn.restype = res
+    if unbound:
+        import sys
+        print(f"[miclip] A/B build {os.environ['MICLIP_LIB']}: entry points left unbound: "
+              f"{', '.join(unbound)}", file=sys.stderr)
     if path is None:
         _lib = lib
     return lib

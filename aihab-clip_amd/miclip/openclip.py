@@ -42,7 +42,7 @@ def list_models():
 
 
 def create_model(model_name, pretrained=None, device="cuda", *, compute_dtype="fp16", seed=0,
-                 **_unused):
+                 allow_seeded=False, **_unused):
     from . import SeededWeightsWarning, load
     from .configs import MODEL_CONFIGS
     if model_name not in OPEN_CLIP_MODELS:
@@ -54,11 +54,18 @@ def create_model(model_name, pretrained=None, device="cuda", *, compute_dtype="f
         src, config = str(pretrained), MODEL_CONFIGS[model_name]
     else:
         if pretrained not in (None, "", "seeded"):
+            # a checkpoint tag: nothing to download offline. Seeded random weights only on
+            # an explicit opt-in -- a filtered warning must never turn into silent
+            # garbage accuracy (round-5 advice)
+            if not allow_seeded:
+                raise RuntimeError(
+                    f"pretrained={pretrained!r} for {model_name}: no pretrained checkpoints are "
+                    f"available offline. Pass a state-dict file path for real weights, or "
+                    f"pretrained='seeded' / allow_seeded=True for SEEDED RANDOM weights.")
             warnings.warn(
                 f"pretrained={pretrained!r} for {model_name}: no pretrained checkpoints are "
                 f"available offline; loading SEEDED RANDOM weights (seed={seed}) of the "
-                f"{model_name} shapes. Pass a state-dict file path for real weights.",
-                SeededWeightsWarning, stacklevel=3)
+                f"{model_name} shapes (allow_seeded=True).", SeededWeightsWarning, stacklevel=2)
         src, config = model_name, None
     with warnings.catch_warnings():
         # the tag warning above (or the explicit None / "seeded") already said it

@@ -357,8 +357,10 @@ int miclip_op_attention(int32_t dtype, const void* qkv, void* out, int32_t B, in
 /* conv1 patchify as the patch GEMM's A operand (clip/model.py:217-219): images
  * [B, 3, R, R] (image_dtype MICLIP_F32 / FP16 / BF16) -> patches [B*(R/P)^2, Kp]
  * (dtype FP16 / BF16), column c*P*P + ky*P + kx, zero up to Kp (>= 3*P*P). variant 0 =
- * default (one workgroup per band of R/P patches where R % 4 == 0 and Kp % 4 == 0, else
- * 1), 1 = one workgroup per patch. Bit-identical. */
+ * default (one workgroup per band of R/P patches -- 16-B vector loads and stores -- where
+ * R % 4 == 0, Kp % 4 == 0 and `images` and `patches` are 16-byte aligned, else 1), 1 = one
+ * workgroup per patch (element accesses, no alignment requirement). Bit-identical. The
+ * encode entry points take any alignment the same way. */
 int miclip_op_im2col(int32_t dtype, int32_t image_dtype, const void* images, void* patches,
                      int32_t B, int32_t R, int32_t P, int32_t Kp, int32_t variant, void* stream);
 

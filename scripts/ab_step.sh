@@ -5,7 +5,7 @@
 #   OUT=name R=3 bash scripts/ab_step.sh tests/test_x.py ...
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-export TMPDIR=/tmp MICLIP_QUIET=1
+export TMPDIR=/tmp MICLIP_QUIET=1 MICLIP_AB_BUILD=1
 O=gpurun_out/${OUT:-ab}
 mkdir -p $O
 if [ $# -gt 0 ]; then

@@ -3,7 +3,7 @@
 # interleaved rounds), then the same-box step A/B (scripts/ab_step.sh).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-export TMPDIR=/tmp MICLIP_QUIET=1
+export TMPDIR=/tmp MICLIP_QUIET=1 MICLIP_AB_BUILD=1
 O=gpurun_out/${OUT:-attn}
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_kernels.py tests/test_gpu_parity.py > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }

@@ -6,7 +6,7 @@
 #   OUT=name BATCHES="256 128 64 32 16" EXTRA="--ab-splits" [LIB=other.so] bash scripts/strong_sweep.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-export TMPDIR=/tmp MICLIP_QUIET=1
+export TMPDIR=/tmp MICLIP_QUIET=1 MICLIP_AB_BUILD=1
 O=gpurun_out/${OUT:-strong}
 mkdir -p $O
 for b in ${BATCHES:-256 128 64 32 16}; do

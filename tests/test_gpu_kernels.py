@@ -423,6 +423,16 @@ def test_attention_dh80_pipelined(lib, dt, N):
         torch.cuda.synchronize()
         assert torch.equal(big[:B * N], ref), f"{(big[:B * N] != ref).sum().item()} elements differ"
         assert bool((big[B * N] == 7.0).all())
+    # a short last workgroup: 143 images = 2288 heads, hpw = 9 over 255 workgroups, the
+    # last one with nh = 2 (its ring and the partial merge stop early)
+    Bs = 143
+    short = torch.full((Bs * N + 1, H * 80), 7.0, device="cuda", dtype=tdt)
+    _check(lib, lib.miclip_op_attention(code, qkv.data_ptr(), short.data_ptr(), Bs, N, H, 80, 0, 6,
+                                        _stream()))
+    torch.cuda.synchronize()
+    assert torch.equal(short[:Bs * N], ref[:Bs * N]), \
+        f"{(short[:Bs * N] != ref[:Bs * N]).sum().item()} elements differ"
+    assert bool((short[Bs * N] == 7.0).all())
     for bad_n, causal in ((255, 0), (260, 0), (257, 1)):
         assert lib.miclip_op_attention(code, qkv.data_ptr(), big.data_ptr(), 1, bad_n, H, 80, causal,
                                        6, _stream()) != 0

@@ -181,8 +181,8 @@ def test_create_model_from_state_dict_file(golden, tmp_path):
     """pretrained=<file>: the ViT-H-14 state dict saved and reloaded through
     open_clip.create_model builds the named config (exact GELU, 16 heads of 80),
     not build_model's inference (QuickGELU, 64-wide heads): features equal the
-    seeded model's bit for bit. A pretrained TAG loads the seeded weights with a
-    SeededWeightsWarning (no checkpoints offline)."""
+    seeded model's bit for bit. A pretrained TAG (no checkpoints offline) raises unless
+    allow_seeded=True, which loads the seeded weights with a SeededWeightsWarning."""
     import open_clip
     g = golden("vith14")
     ref = _model("fp16")
@@ -194,8 +194,11 @@ def test_create_model_from_state_dict_file(golden, tmp_path):
     assert torch.equal(m.encode_image(imgs), ref.encode_image(imgs))
     del m
     import miclip
+    with pytest.raises(RuntimeError, match="no pretrained checkpoints"):
+        open_clip.create_model("ViT-H-14", pretrained="laion2b_s32b_b79k")
     with pytest.warns(miclip.SeededWeightsWarning, match="SEEDED RANDOM"):
-        tagged = open_clip.create_model("ViT-H-14", pretrained="laion2b_s32b_b79k")
+        tagged = open_clip.create_model("ViT-H-14", pretrained="laion2b_s32b_b79k",
+                                        allow_seeded=True)
     assert torch.equal(tagged.encode_image(imgs), ref.encode_image(imgs))
     del tagged
     with pytest.raises(NotImplementedError):

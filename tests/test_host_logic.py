@@ -94,9 +94,9 @@ def test_preprocess_shapes():
 
 
 def test_openclip_pretrained_rules():
-    """open_clip.create_model: a checkpoint tag (no checkpoints offline) loads the
-    seeded weights with a SeededWeightsWarning -- never silently -- the same policy as
-    miclip.load(<model name>) (round-4 advice); an unknown model
+    """open_clip.create_model: a checkpoint tag (no checkpoints offline) raises unless
+    the caller opts in (allow_seeded=True), and then loads the seeded weights with a
+    SeededWeightsWarning -- never silently (round-5 advice); an unknown model
     raises like open_clip; a state-dict file is checked against the NAMED config
     (ViT-H-14: GELU, 80-wide heads), which build_model's inference cannot see."""
     from types import SimpleNamespace
@@ -112,10 +112,16 @@ def test_openclip_pretrained_rules():
     miclip.load = fake_load
     try:
         for tag in ("openai", "laion2b_s32b_b79k"):
+            with pytest.raises(RuntimeError, match="no pretrained checkpoints"):
+                create_model("ViT-H-14", pretrained=tag, device="cpu")
+            assert not captured
             with pytest.warns(miclip.SeededWeightsWarning, match="SEEDED RANDOM"):
                 with pytest.raises(RuntimeError, match="stop before the GPU"):
-                    create_model("ViT-H-14", pretrained=tag, device="cpu")
+                    create_model("ViT-H-14", pretrained=tag, device="cpu", allow_seeded=True)
             assert captured["src"] == "ViT-H-14" and captured["config"] is None
+            captured.clear()
+        with pytest.raises(RuntimeError, match="stop before the GPU"):
+            create_model("ViT-H-14", pretrained="seeded", device="cpu")
     finally:
         miclip.load = real
     with pytest.raises(RuntimeError, match="not found"):
