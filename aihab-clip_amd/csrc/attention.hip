@@ -395,6 +395,190 @@ MICLIP_DEV void attend_extra_keys(const char* kimg, const char* vimg, const i16x
   }
 }
 
+// Full key tiles [kt0, kt1) of one wave's 32 queries with the softmax's per-element
+// VALU work moved onto the matrix pipe (the x8, one-head N = 577 and head-dim-80
+// kernels; they were VALU-bound: r04 PMC 22 % MFMA busy at 17 VALU per MFMA, the
+// tile loop issuing ~75 VALU + 16 v_exp per 8 MFMAs):
+//  * Q arrives pre-scaled by c2 = scale * log2(e) (prescale_q: one fp32 product and
+//    one rounding per element, once per chunk), so S' = K . Q'^T is already in the
+//    base-2 softmax domain;
+//  * the running max leaves through the MFMA chain: every tile's S' chain starts
+//    with a shift k-step ones . (-m~)^T (A = 1 in k-slot 0 of the first lane half,
+//    B = -m~ rounded to the compute dtype there, zeros elsewhere), so the
+//    accumulator holds S' - m~ and p = exp2(acc) takes no per-element FMA (m~ only
+//    has to be one shift per row: p, l and O all use it);
+//  * the lazy-rescale test is one v_max3 tree against the threshold per lane (the
+//    wave vote covers both lane halves; no lane exchange on the fast path);
+//  * the row sum is a v_dot2 of the rounded P pairs with ones -- the sum of exactly
+//    the P values the P.V MFMAs use -- 8 ops instead of 16 adds;
+//  * NT > 0: the NT tiles are unrolled, every LDS read a per-lane base + immediate.
+// PIPE: tile kt+1's S MFMAs are issued before tile kt's softmax (a max update in
+// tile kt then corrects the in-flight tile by the same shift). `fresh`: the first
+// call of a chunk (o, l zeroed; m~ set from the first tile's max). Leaves the
+// unnormalised O^T, this lane's partial row sum (reduce across the lane halves
+// after any further keys) and m~ (scaled log2 domain: attend_extra_keys with c2 = 1).
+// tile0: the key tile held at byte 0 of kimg / vimg. All tiles must be full (no
+// masking: kt1 * 32 <= N, not causal).
+template <typename T, class G>
+MICLIP_DEV void prescale_q(i16x8 (&qf)[G::NKS], float c2) {
+#pragma unroll
+  for (int s = 0; s < G::NKS; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qf[s][j] = to_bits<T>(from_bits<T>(qf[s][j]) * c2);
+}
+
+template <typename T, class G, bool PIPE, int NT = 0>
+MICLIP_DEV void attend_shift(const char* kimg, const char* vimg, const i16x8 (&qf)[G::NKS],
+                             int lane, f32x16 (&o)[G::NDT], float& lsum, float& m, int kt0,
+                             int kt1, bool fresh, int tile0 = 0) {
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+  unsigned kb = (unsigned)(uintptr_t)(const LDS_AS char*)kimg;
+  unsigned vb = (unsigned)(uintptr_t)(const LDS_AS char*)vimg;
+  asm("" : "+s"(kb), "+s"(vb));
+  const LDS_AS char* kp[G::NKS];
+#pragma unroll
+  for (int s = 0; s < G::NKS; ++s)
+    kp[s] = (const LDS_AS char*)(uintptr_t)(kb + l32 * G::ROWB + (G::kswz(2 * s + hh, l32) << 4));
+  const LDS_AS char* vp[G::NDT];
+#pragma unroll
+  for (int dt = 0; dt < G::NDT; ++dt) {
+    int ch = 4 * dt + 2 * (g & 1) + (tp >> 1);
+    if (ch >= G::CH) ch -= 2;   // HeadGeom80u: dims 80-95 re-read 64-79 (never stored)
+    const int vr = 4 * (g >> 1) + tq;
+    vp[dt] = (const LDS_AS char*)(uintptr_t)(vb + vr * G::ROWB + (G::vswz(ch, vr) << 4) + 8 * (tp & 1));
+  }
+  const short one = to_bits<T>(1.0f);
+  const i16x8 ka = {hh == 0 ? one : (short)0, 0, 0, 0, 0, 0, 0, 0};
+  i16x8 qm = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint32_t ones2 = (uint32_t)(unsigned short)one * 0x10001u;
+  if (fresh) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+      for (int dt = 0; dt < G::NDT; ++dt) o[dt][r] = 0.f;
+    lsum = 0.f;
+    m = 0.f;
+  } else {
+    qm[0] = hh == 0 ? to_bits<T>(-m) : (short)0;
+  }
+  auto qk = [&](int kt, f32x16& sacc) {
+    const int off = (kt - tile0) * G::TILEB;
+    __builtin_amdgcn_s_setprio(1);
+    const i16x8 k0 = *(const LDS_AS i16x8*)(kp[0] + off);
+    sacc = Mfma<T>::m32(ka, qm, f32x16{});
+    sacc = Mfma<T>::m32(k0, qf[0], sacc);
+#pragma unroll
+    for (int s = 1; s < G::NKS; ++s) {
+      const i16x8 kf = *(const LDS_AS i16x8*)(kp[s] + off);
+      sacc = Mfma<T>::m32(kf, qf[s], sacc);
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // nxt: the tile in flight behind this one (PIPE), corrected by a max update when
+  // has_nxt (a reference, never a pointer: a pointer to one of two register tiles
+  // picked at run time put both in scratch)
+  auto softmax_pv = [&](int kt, f32x16& sacc, f32x16& nxt, bool has_nxt) {
+    const float t0 = fmaxf(fmaxf(sacc[0], sacc[1]), sacc[2]);
+    const float t1 = fmaxf(fmaxf(sacc[3], sacc[4]), sacc[5]);
+    const float t2 = fmaxf(fmaxf(sacc[6], sacc[7]), sacc[8]);
+    const float t3 = fmaxf(fmaxf(sacc[9], sacc[10]), sacc[11]);
+    const float t4 = fmaxf(fmaxf(sacc[12], sacc[13]), sacc[14]);
+    const float tmax = fmaxf(fmaxf(fmaxf(t0, t1), t2), fmaxf(fmaxf(t3, t4), sacc[15]));
+    if (fresh || !__all(tmax <= 8.0f)) {
+      // first tile of the chunk, or a tile max more than 2^8 above m~: m~ = the row
+      // max (both lane halves), rounded to the compute dtype; O and l rescaled
+      const float rmax = xor32_max(tmax) + m;   // absolute, scaled log2 domain
+      const float mn = from_bits<T>(to_bits<T>(fresh ? rmax : fmaxf(m, rmax)));
+      const float d = mn - m;
+      if (!fresh) {
+        const float alpha = __builtin_amdgcn_exp2f(-d);
+        lsum *= alpha;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+#pragma unroll
+          for (int dt = 0; dt < G::NDT; ++dt) o[dt][r] *= alpha;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[r] -= d;
+      if (has_nxt) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) nxt[r] -= d;
+      }
+      m = mn;
+      qm[0] = hh == 0 ? to_bits<T>(-mn) : (short)0;
+      fresh = false;
+    }
+    i16x8 pf[2];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sacc[r] = __builtin_amdgcn_exp2f(sacc[r]);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pf[s2][j] = to_bits<T>(sacc[8 * s2 + j]);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const u32x4 w = __builtin_bit_cast(u32x4, pf[s2]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) lsum = dot2acc<T>(w[e], ones2, lsum);
+    }
+    const int off = (kt - tile0) * G::TILEB;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+      for (int dt = 0; dt < G::NDT; ++dt) {
+        const LDS_AS char* a0 = vp[dt] + off + 16 * G::ROWB * s2;
+        const i16x4 lo = ds_read_tr16_b64(a0);
+        const i16x4 hi = ds_read_tr16_b64(a0 + 8 * G::ROWB);
+        const i16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[dt] = Mfma<T>::m32(vf, pf[s2], o[dt]);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  if constexpr (NT > 0) {
+    if constexpr (PIPE) {
+      f32x16 sa, sb;
+      qk(kt0, sa);
+#pragma unroll
+      for (int i = 0; i < NT; i += 2) {
+        if (i + 1 < NT) qk(kt0 + i + 1, sb);
+        softmax_pv(kt0 + i, sa, sb, i + 1 < NT);
+        if (i + 1 < NT) {
+          if (i + 2 < NT) qk(kt0 + i + 2, sa);
+          softmax_pv(kt0 + i + 1, sb, sa, i + 2 < NT);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        f32x16 sa;
+        qk(kt0 + i, sa);
+        softmax_pv(kt0 + i, sa, sa, false);
+      }
+    }
+  } else if constexpr (PIPE) {
+    f32x16 sa, sb;
+    int kt = kt0;
+    if (kt < kt1) qk(kt, sa);
+    for (; kt + 2 <= kt1; kt += 2) {
+      qk(kt + 1, sb);
+      softmax_pv(kt, sa, sb, true);
+      const bool more = kt + 2 < kt1;
+      if (more) qk(kt + 2, sa);
+      softmax_pv(kt + 1, sb, sa, more);
+    }
+    if (kt < kt1) softmax_pv(kt, sa, sb, false);
+  } else {
+    for (int kt = kt0; kt < kt1; ++kt) {
+      f32x16 sa;
+      qk(kt, sa);
+      softmax_pv(kt, sa, sa, false);
+    }
+  }
+}
+
 template <typename T, int DH>
 MICLIP_DEV void attend_store(const f32x16 (&o)[HeadGeom<DH>::NDT], float lsum, int chunk, int N,
                              T* op_row0, int D, int lane) {
@@ -525,9 +709,10 @@ __global__ __launch_bounds__(NWMAX * 64) void attention_kernel(
     float lsum, m;
     if constexpr (DH == 64 && !CAUSAL) {
       if (xkeys) {
-        attend_chunk<T, CAUSAL, DH>(kimg, vimg, qf, chunk, N, Npad, c2, lane, o, lsum, m, 0,
-                                    nfull, prio, true, false);
-        attend_extra_keys<T>(kimg, vimg, qf, o, lsum, m, 32 * nfull, nextra, c2, lane);
+        // Q in the base-2 softmax domain (attend_shift); the extra keys take c2 = 1
+        prescale_q<T, G>(qf, c2);
+        attend_shift<T, G, true>(kimg, vimg, qf, lane, o, lsum, m, 0, nfull, true);
+        attend_extra_keys<T>(kimg, vimg, qf, o, lsum, m, 32 * nfull, nextra, 1.0f, lane);
         lsum = xor32_sum(lsum);
         attend_store<T, DH>(o, lsum, chunk, N, out + (size_t)b * N * D + h * DH, D, lane);
         continue;
@@ -832,6 +1017,7 @@ __global__ __launch_bounds__(512) void attention80p_kernel(const T* __restrict__
                  : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]), "+v"(qf[4])
                  :
                  : "memory");
+    prescale_q<T, G>(qf, c2);   // the full chunk runs in the base-2 domain (attend_shift)
   }
   __builtin_amdgcn_s_barrier();
   for (int j = 0; j < nh; ++j) {
@@ -857,8 +1043,7 @@ __global__ __launch_bounds__(512) void attention80p_kernel(const T* __restrict__
     }
     f32x16 o[3];
     float lsum, m;
-    attend_chunk<T, false, 80, true, false, G>(ia, ia + HALFB, qf, wave, N, 256, c2, olane(), o, lsum,
-                                               m, 0, 4, prio, true, false, 0);
+    attend_shift<T, G, true, 4>(ia, ia + HALFB, qf, olane(), o, lsum, m, 0, 4, true, 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     // ---- second half: key tiles 4-7 in slot sb. Unit (j+1, 1) -> slot sa (just
@@ -870,9 +1055,8 @@ __global__ __launch_bounds__(512) void attention80p_kernel(const T* __restrict__
     }
     const char* ib = smem + sb * SLOTB;
     const char* ix = ximg + (j & 1) * 3072;
-    attend_chunk<T, false, 80, true, false, G>(ib, ib + HALFB, qf, wave, N, 256, c2, olane(), o, lsum,
-                                               m, 4, 8, prio, false, false, 4);
-    if (nvalid > 0) attend_extra_keys80u<T>(ix, ix + 1024, qf, o, lsum, m, nvalid, c2, olane());
+    attend_shift<T, G, true, 4>(ib, ib + HALFB, qf, olane(), o, lsum, m, 4, 8, false, 4);
+    if (nvalid > 0) attend_extra_keys80u<T>(ix, ix + 1024, qf, o, lsum, m, nvalid, 1.0f, olane());
     lsum = xor32_sum(lsum);
     if (more) {
       // hipcc waits for these loads here (vmcnt(0): nothing younger is visible to
@@ -881,6 +1065,7 @@ __global__ __launch_bounds__(512) void attention80p_kernel(const T* __restrict__
 #pragma unroll
       for (int s = 0; s < 5; ++s) qf[s] = qn[s];
       asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]), "+v"(qf[4]));
+      prescale_q<T, G>(qf, c2);
     }
     attend_store<T, 80>(o, lsum, wave, N, out + (size_t)b * N * D + h * 80, D, lane);
     if (nvalid > 0 && wave >= 4) {
@@ -1050,142 +1235,6 @@ __global__ __launch_bounds__(SPLIT ? 512 : 640) void attention_pipe_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// The x8 kernel's full query chunk: one wave's 32 queries against key tiles 0..7
-// (keys 0..255, never masked), with the softmax's VALU work moved onto the matrix
-// pipe. The kernel is VALU-bound at N = 257 (r04 PMC: 22 % MFMA busy at 17 VALU per
-// MFMA; the tile loop issued ~75 VALU + 16 v_exp per 8 MFMAs). Here:
-//  * Q arrives pre-scaled by c2 = scale * log2(e) (prescale_q: one fp32 product
-//    and one rounding per element, once per head), so S' = K . Q'^T is already in
-//    the base-2 softmax domain;
-//  * the running max leaves through the MFMA chain: each tile's S' chain starts
-//    from a fifth k-step ones . (-m~)^T (A = ones in k-slot 0 of the lanes' first
-//    8-half group, B = -m~ rounded to the compute dtype), so the accumulator holds
-//    S' - m~ and p = exp2(acc) needs no per-element FMA (m~ only has to be the same
-//    shift for every p of the row: p, l and O all use it);
-//  * the lazy-rescale test is one v_max3 tree against the threshold, per lane (the
-//    wave-wide vote covers both lane halves, no lane exchange on the fast path);
-//  * the row sum is a v_dot2 of the rounded P pairs with ones (the sum of exactly
-//    the P values the P.V MFMAs use), 8 ops instead of 16 adds;
-//  * the 8 tiles are unrolled: every LDS read is a per-lane base + an immediate.
-// Tile 0 finds the first max with the full reduction (m starts undefined).
-// Leaves the unnormalised O^T, this lane's partial row sum (reduce across the lane
-// halves after any further keys) and m~ (scaled log2 domain) for attend_extra_keys.
-// ---------------------------------------------------------------------------
-template <typename T>
-MICLIP_DEV void prescale_q(i16x8 (&qf)[4], float c2) {
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) qf[s][j] = to_bits<T>(from_bits<T>(qf[s][j]) * c2);
-}
-
-template <typename T>
-MICLIP_DEV void attend_full_x8(const char* kimg, const char* vimg, const i16x8 (&qf)[4], int lane,
-                               f32x16 (&o)[2], float& lsum, float& m) {
-  using G = HeadGeom<64>;
-  const int l32 = lane & 31, hh = lane >> 5;
-  const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
-  unsigned kb = (unsigned)(uintptr_t)(const LDS_AS char*)kimg;
-  unsigned vb = (unsigned)(uintptr_t)(const LDS_AS char*)vimg;
-  asm("" : "+s"(kb), "+s"(vb));
-  const LDS_AS char* kp[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-    kp[s] = (const LDS_AS char*)(uintptr_t)(kb + l32 * G::ROWB + (G::kswz(2 * s + hh, l32) << 4));
-  const LDS_AS char* vp[2];
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt) {
-    const int ch = 4 * dt + 2 * (g & 1) + (tp >> 1), vr = 4 * (g >> 1) + tq;
-    vp[dt] = (const LDS_AS char*)(uintptr_t)(vb + vr * G::ROWB + (G::vswz(ch, vr) << 4) + 8 * (tp & 1));
-  }
-  // the shift k-step: A[key][k] = (k == 0), B[k][query] = -m~ (k == 0): lanes of the
-  // first half hold k-slots 0..7 (hh = 0), so only their first element is non-zero
-  const short one = to_bits<T>(1.0f);
-  const i16x8 ka = {hh == 0 ? one : (short)0, 0, 0, 0, 0, 0, 0, 0};
-  i16x8 qm = {0, 0, 0, 0, 0, 0, 0, 0};
-  const uint32_t ones2 = (uint32_t)(unsigned short)one * 0x10001u;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    o[0][r] = 0.f;
-    o[1][r] = 0.f;
-  }
-  lsum = 0.f;
-  m = 0.f;
-#pragma unroll
-  for (int kt = 0; kt < 8; ++kt) {
-    f32x16 sacc;
-    __builtin_amdgcn_s_setprio(1);
-    if (kt == 0) {
-      const i16x8 kf = *(const LDS_AS i16x8*)(kp[0]);
-      sacc = Mfma<T>::m32(kf, qf[0], f32x16{});
-    } else {
-      const i16x8 kf = *(const LDS_AS i16x8*)(kp[0] + kt * G::TILEB);
-      sacc = Mfma<T>::m32(ka, qm, f32x16{});
-      sacc = Mfma<T>::m32(kf, qf[0], sacc);
-    }
-#pragma unroll
-    for (int s = 1; s < 4; ++s) {
-      const i16x8 kf = *(const LDS_AS i16x8*)(kp[s] + kt * G::TILEB);
-      sacc = Mfma<T>::m32(kf, qf[s], sacc);
-    }
-    __builtin_amdgcn_s_setprio(0);
-    const float t0 = fmaxf(fmaxf(sacc[0], sacc[1]), sacc[2]);
-    const float t1 = fmaxf(fmaxf(sacc[3], sacc[4]), sacc[5]);
-    const float t2_ = fmaxf(fmaxf(sacc[6], sacc[7]), sacc[8]);
-    const float t3 = fmaxf(fmaxf(sacc[9], sacc[10]), sacc[11]);
-    const float t4 = fmaxf(fmaxf(sacc[12], sacc[13]), sacc[14]);
-    const float tmax = fmaxf(fmaxf(fmaxf(t0, t1), t2_), fmaxf(fmaxf(t3, t4), sacc[15]));
-    if (kt == 0 || !__all(tmax <= 8.0f)) {
-      // first tile, or a tile max more than 2^8 above m~: new m~ = the row max
-      // (both lane halves), rounded to the compute dtype; O and l rescaled
-      const float rmax = xor32_max(tmax) + (kt == 0 ? 0.f : m);   // absolute, scaled domain
-      const float mn = from_bits<T>(to_bits<T>(kt == 0 ? rmax : fmaxf(m, rmax)));
-      const float d = mn - m;           // kt > 0: >= 0 up to the rounding of mn
-      if (kt > 0) {
-        const float alpha = __builtin_amdgcn_exp2f(-d);
-        lsum *= alpha;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          o[0][r] *= alpha;
-          o[1][r] *= alpha;
-        }
-      }
-      const float sh = kt == 0 ? mn : d;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[r] -= sh;
-      m = mn;
-      qm[0] = hh == 0 ? to_bits<T>(-mn) : (short)0;
-    }
-    i16x8 pf[2];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sacc[r] = __builtin_amdgcn_exp2f(sacc[r]);
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) pf[s2][j] = to_bits<T>(sacc[8 * s2 + j]);
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const u32x4 w = __builtin_bit_cast(u32x4, pf[s2]);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) lsum = dot2acc<T>(w[e], ones2, lsum);
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        const LDS_AS char* a0 = vp[dt] + kt * G::TILEB + 16 * G::ROWB * s2;
-        const i16x4 lo = ds_read_tr16_b64(a0);
-        const i16x4 hi = ds_read_tr16_b64(a0 + 8 * G::ROWB);
-        const i16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        o[dt] = Mfma<T>::m32(vf, pf[s2], o[dt]);
-      }
-    }
-    __builtin_amdgcn_s_setprio(0);
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Two workgroups per CU (variant 8, default for 8 full query chunks and at most
 // 3 more queries, N in 256..259: ViT-L/14 at 224 px). One workgroup = 8 waves (2 per
 // SIMD) walks hpw (image, head) pairs with ONE K/V buffer (Npad x 256 B, 72 KiB
@@ -1258,8 +1307,8 @@ __global__ __launch_bounds__(512, 4) void attention_x8_kernel(const T* __restric
       f32x16 o[2];
       float lsum, m;
       // Q in the base-2 softmax domain: the full chunk and its extra keys take c2 = 1
-      prescale_q<T>(qf, c2);
-      attend_full_x8<T>(kimg, vimg, qf, lane, o, lsum, m);
+      prescale_q<T, HeadGeom<64>>(qf, c2);
+      attend_shift<T, HeadGeom<64>, false, 8>(kimg, vimg, qf, lane, o, lsum, m, 0, 8, true);
       attend_extra_keys<T>(kimg, vimg, qf, o, lsum, m, 256, nextra, 1.0f, lane);
       lsum = xor32_sum(lsum);
       MICLIP_STAMP(1);   // the wave's full query chunk

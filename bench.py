@@ -203,7 +203,7 @@ class ClockProbe:
     s_memrealtime (100 MHz) before and after; per XCD (HW_REG_XCC_ID)
     delta(memtime) / delta(realtime) x 100 MHz, median over the XCDs."""
 
-    NWG = 64          # 8 per XCD under round-robin dispatch
+    NWG = 512         # 64 per XCD under round-robin dispatch (medians over many CUs)
     MIN_WINDOW_S = 0.1
     GHZ_RANGE = (1.0, 2.4)   # MI355X core clock floor under load .. nameplate maximum
 
