@@ -24,9 +24,9 @@ __all__ = ["available_models", "load", "tokenize", "build_model", "CLIP", "CLIPC
 
 
 class SeededWeightsWarning(UserWarning):
-    """A model name (or an open_clip pretrained tag) was resolved to seeded random
-    weights: no checkpoints exist offline. Filter it where that is intended
-    (benchmarks, tests); pass a state-dict path for real weights."""
+    """A model name (or, with allow_seeded=True, an open_clip pretrained tag) was
+    resolved to seeded random weights: no checkpoints exist offline. Filter it where
+    that is intended (benchmarks, tests); pass a state-dict path for real weights."""
 
 
 def _transform(n_px):
@@ -40,7 +40,7 @@ def load(name, device="cuda" if torch.cuda.is_available() else "cpu", jit=False,
 
     `name` is a model name from available_models() -- resolved offline to the
     CLIP shapes with seeded random weights (no checkpoints exist offline; a
-    SeededWeightsWarning says so, as for an open_clip pretrained tag) -- or
+    SeededWeightsWarning says so) -- or
     a path to a state-dict checkpoint (loaded with weights_only=True). Anything
     else raises RuntimeError like the reference. `jit=True` is accepted with a
     warning and loads the non-JIT model (the reference does the same when the
