@@ -37,6 +37,8 @@ stamps: $(OBJS)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) build/stamps/stamp_attn.o $(filter-out $(OBJ_DIR)/attention.o,$(OBJS)) -o build/stamps/libstamp_attn.so
 	$(HIPCC) $(HIPFLAGS) -c scripts/stamps/stamp_gemm_kloop.hip -o build/stamps/stamp_gemm_kloop.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) build/stamps/stamp_gemm_kloop.o $(filter-out $(OBJ_DIR)/gemm.o,$(OBJS)) -o build/stamps/libstamp_gemm_kloop.so
+	$(HIPCC) $(HIPFLAGS) -c scripts/stamps/stamp_gemm_kphase.hip -o build/stamps/stamp_gemm_kphase.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) build/stamps/stamp_gemm_kphase.o $(filter-out $(OBJ_DIR)/gemm.o,$(OBJS)) -o build/stamps/libstamp_gemm_kphase.so
 
 # timing diagnostics (outputs meaningless): the library without the vision-tower
 # attention / without the large ln_stats launches, to price what each costs inside

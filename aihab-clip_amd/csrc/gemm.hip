@@ -40,6 +40,12 @@
 #define MICLIP_KSTAMP(i)
 #define MICLIP_ESTAMP(i) MICLIP_STAMP(i)
 #endif
+// MICLIP_STAMPS_KPHASE (scripts/stamps/stamp_gemm_kphase.hip): the parts of each
+// main-loop phase as segments (MICLIP_PSTAMP; that build folds every other stamp
+// into segment 0)
+#ifndef MICLIP_PSTAMP
+#define MICLIP_PSTAMP(i)
+#endif
 
 namespace miclip {
 
@@ -1123,6 +1129,7 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
       const char* sB1 = smem + (buf * 4 + 3) * HALF + boff;
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
+        MICLIP_PSTAMP(7);   // the previous phase's closing barrier
         if (p == 0 && wr == 0 && t > 0) {
           MICLIP_KSTAMP(1);
           if (t + 1 < nk) {
@@ -1148,14 +1155,20 @@ __global__ __launch_bounds__(512) void gemm256s_kernel(const T* __restrict__ A,
         }
         const int qi = (p >= 2) ? 1 : 0;
         const int qj = (p == 1 || p == 2) ? 1 : 0;
+        MICLIP_PSTAMP(6);   // vmcnt wait
         quadrant(qi ? sA1 : sA0, qj ? sB1 : sB0, p == 0 || p == 2, p != 2);
+        MICLIP_PSTAMP(1);   // fragment reads (the stamp waits for them)
         if (p == 0 && t + 1 < nk) stage(1, t + 1);
         if (p == 1 && t + 1 < nk) stage(2, t + 1);
         if (p == 2 && t + 2 < nk) stage(0, t + 2);
         if (p == 3 && t + 2 < nk) stage(3, t + 2);
+        MICLIP_PSTAMP(2);   // LDS-DMA issue
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        MICLIP_PSTAMP(3);
         lds_barrier();
+        MICLIP_PSTAMP(4);   // barrier before the MFMAs
         mfma_q(qi, qj, first_c);
+        MICLIP_PSTAMP(5);   // MFMA issue
         lds_barrier();
       }
     };

@@ -25,6 +25,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 SEGS = {
     "gemm": ["tile_top", "main_loop", "boundary", "epilogue", "row_tail", "epi_math_stage",
              "epi_barrier", "epi_readback_store"],
+    "gemm_phases": ["outside_k_loop", "frag_reads", "dma_issue", "lgkm_wait", "barrier_pre_mfma",
+                    "mfma_issue", "vmcnt_wait", "barrier_close"],
     "attn": ["kv_load_wait", "chunk", "store", "ragged", "close_barrier", "merge", "dma_issue",
              "q_load_and_wait"],
 }
@@ -39,6 +41,8 @@ def main():
     ap.add_argument("--n", type=int, default=257)
     ap.add_argument("--warm", type=int, default=5)
     ap.add_argument("--null", action="store_true", help="gemm: the no-output epilogue (epi 3)")
+    ap.add_argument("--phases", action="store_true",
+                    help="gemm: segment names of the K-loop phase build (libstamp_gemm_kphase.so)")
     args = ap.parse_args()
     lib = ctypes.CDLL(os.environ.get("STAMP_LIB") or
                       os.path.join(ROOT, "build", "stamps", f"libstamp_{args.kernel}.so"))
@@ -97,7 +101,7 @@ def main():
     rec = rec[rec[:, 8] > 0].astype(np.float64)       # waves that ran
     tot = rec[:, 8]
     clock = tot / (rec[:, 9] / 100e6)                   # cycles per second
-    names = SEGS[args.kernel]
+    names = SEGS["gemm_phases" if args.kernel == "gemm" and args.phases else args.kernel]
     segs = {n: dict(mean_cycles=round(float(rec[:, i].mean())),
                     share=round(float(rec[:, i].sum() / tot.sum()), 4))
             for i, n in enumerate(names)}
