@@ -46,3 +46,25 @@ def test_sharded_encode_rccl_world1():
         assert torch.equal(feats, ref) and torch.equal(labels.cpu(), torch.arange(37))
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_sharded_cache_gloo_world2_one_gpu():
+    """Two ranks (torch.distributed.run, gloo over 127.0.0.1) share the one GPU of the
+    box, each running its own HIP model on cuda:0: the sharded encode and both
+    sharded feature-cache loader forms equal the single-process encode bit for bit
+    on every rank (tests/dist_gpu_worker.py). The ranks are started as child
+    processes (no exec from this GPU-initialised process)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(root, "tests", "dist_gpu_worker.py")]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    assert "RANK_OK 0" in out and "RANK_OK 1" in out, out[-3000:]
