@@ -61,6 +61,10 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"])
+    ap.add_argument("--rehearse-gloo", action="store_true",
+                    help="one-GPU rehearsal of the N-rank logic: gloo collectives, every rank on "
+                         "cuda:(LOCAL_RANK mod devices); the line is marked, its value is not a "
+                         "multi-GPU result")
     ap.add_argument("--no-weak", action="store_true",
                     help="N > 1 strong runs: skip the secondary weak-scaling measurement")
     ap.add_argument("--model", default="ViT-L/14")
@@ -251,13 +255,16 @@ def run(args, backend="nccl", load_model=None):
     import torch
     import torch.distributed as dist
 
-    on_gpu = backend == "nccl"
+    rehearse = bool(getattr(args, "rehearse_gloo", False))
+    on_gpu = backend == "nccl" or rehearse
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if on_gpu:
+        if rehearse:
+            dist.init_process_group("gloo")
+        elif on_gpu:
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         else:
             dist.init_process_group(backend)
@@ -266,6 +273,8 @@ def run(args, backend="nccl", load_model=None):
     if args.gpus != world and rank == 0:
         log(f"[bench] --gpus {args.gpus} but the process group has {world} ranks; reporting {world}")
     if on_gpu:
+        if rehearse:
+            local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
         dev = torch.device(f"cuda:{local}")
     else:
@@ -351,7 +360,7 @@ def run(args, backend="nccl", load_model=None):
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
-        dt_t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dt_t = torch.tensor([dt], device="cpu" if rehearse else dev, dtype=torch.float64)
         if world > 1:
             dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
         return float(dt_t.item())
@@ -539,6 +548,9 @@ def run(args, backend="nccl", load_model=None):
             "clock_ghz": clock_ghz,
             "roofline": roofline, "cpu_baseline": cpu, "kernels": kernels,
         }
+        if rehearse:
+            line["rehearsal"] = (f"{world} ranks over gloo on {torch.cuda.device_count()} GPU(s): "
+                                 "the multi-rank logic on hardware, not a scaling result")
         if ab:
             line["splits_ab_img_s"] = ab
         if abf:

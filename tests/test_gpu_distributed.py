@@ -68,3 +68,29 @@ def test_sharded_cache_gloo_world2_one_gpu():
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-3000:]
     assert "RANK_OK 0" in out and "RANK_OK 1" in out, out[-3000:]
+
+
+@pytest.mark.timeout(300)
+def test_bench_two_rank_rehearsal():
+    """bench.py's N-rank logic on the box (the driver's 8-GPU run is not ours to start):
+    torch.distributed.run with two ranks, gloo collectives, both ranks on the one GPU
+    (--rehearse-gloo). Rank 0 prints one JSON line for the world of 2, marked as a
+    rehearsal; the step's guard against the single-GPU encode ran on both ranks."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="4", MICLIP_QUIET="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(root, "bench.py"), "--gpus", "2", "--rehearse-gloo", "--model", "ViT-B/32",
+           "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280, cwd=root)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 3 and d["value"] > 0 and "rehearsal" in d
+    assert d["config"]["global_batch"] == 256 and d["config"]["images_per_gpu"] == 128
